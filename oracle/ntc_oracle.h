@@ -1,0 +1,135 @@
+/*
+ * ntc_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of ahamez/netcode's GF(2^8) coding path (reference at /root/reference, read
+ * only).  This is the *checker*: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load it.  The product (netcode_amd/, libntc_gf256.so) never links or calls it.
+ *
+ * Parity pins (see DESIGN.md "Oracle"):
+ *   - GF(2^8) polynomial 0x11D (gf-complete's w=8 default; the reference calls gf_init_easy(&gf,8)
+ *     at netcode/detail/galois_field.hh:40 and never names the polynomial).
+ *   - SURVEY.md §8(c) hand-checked KATs (wire bytes of a 2-source repair, scalar coefficients,
+ *     inverses) and SURVEY.md §6 end_to_end golden counters (reference compiled in the survey
+ *     container, 1000 and 10000 packets).
+ *   - tests/netcode/detail/test_invert_matrix.cc (jerasure inverse equality, singular 3x3).
+ */
+#ifndef NTC_ORACLE_H
+#define NTC_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- GF(2^8) / 0x11D ---------- */
+uint8_t  or_gf_mul(uint8_t a, uint8_t b);
+uint8_t  or_gf_inv(uint8_t a);                     /* a != 0 */
+uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id);   /* galois_field.hh:143-158, w=8 */
+void     or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
+void     or_region_muladd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
+uint16_t or_multiply_size(uint16_t size, uint32_t c);           /* galois_field.hh:96-120 */
+
+/* Jerasure Gauss-Jordan on a column-major square_matrix (invert_matrix.cc:9-128).
+ * Returns -1 on success, else the failure index the reference returns (rows-1). */
+long     or_invert(uint32_t* mat, uint32_t* inv, size_t n);
+
+/* -------------------------------------------------------- generation encode (batch form) ---- */
+/* One generation: R_j = sum_i c(rid_base+j, sid_base+i) * X_i, sources zero padded to `stride`
+ * (detail/encoder.cc:15-64).  src: [k][stride], rep: [r][stride]; rep_size[j] = encoded size. */
+void or_encode_generation(uint32_t k, uint32_t r, uint32_t stride, const uint8_t* src,
+                          const uint16_t* src_len, uint32_t sid_base, uint32_t rid_base,
+                          uint8_t* rep, uint16_t* rep_size, uint16_t* rep_len);
+
+/* Batch encode over G generations, optional OpenMP-free pthread fan-out (nthreads >= 1). */
+void or_encode_batch(uint32_t G, uint32_t k, uint32_t r, uint32_t stride, const uint8_t* src,
+                     const uint16_t* src_len, const uint32_t* sid_base, const uint32_t* rid_base,
+                     uint8_t* rep, uint16_t* rep_size, int use_simd, int nthreads);
+
+/* -------------------------------------------------------- generation decode (batch form) ---- */
+/* Per-generation result of feeding the received sources (ascending id) then the received
+ * repairs (ascending id) of one generation into a fresh reference decoder
+ * (detail/decoder.cc:33-152, 412-566). */
+typedef struct {
+  uint8_t  state;          /* 0 decoded, 1 nothing missing, 2 not enough repairs, 3 singular */
+  uint8_t  nb_failed;      /* nb_failed_full_decodings */
+  uint16_t nb_missing;     /* m */
+  uint16_t nb_decoded;     /* nb_decoded */
+  uint16_t nb_useless;     /* nb_useless_repairs */
+  uint16_t last_repair;    /* index (in the generation) of the repair that completed decoding */
+  uint16_t pad;
+} or_decode_status;
+
+/* src: [k][stride] in/out (lost slots receive recovered payloads zero-padded to stride);
+ * src_len in/out; rep: [r][stride]; rep_size: encoded sizes; masks: 1 = received. */
+void or_decode_generation(uint32_t k, uint32_t r, uint32_t stride, uint8_t* src, uint16_t* src_len,
+                          const uint8_t* src_mask, const uint8_t* rep, const uint16_t* rep_size,
+                          const uint16_t* rep_len, const uint8_t* rep_mask, uint32_t sid_base,
+                          uint32_t rid_base, or_decode_status* st);
+
+void or_decode_batch(uint32_t G, uint32_t k, uint32_t r, uint32_t stride, uint8_t* src,
+                     uint16_t* src_len, const uint8_t* src_mask, const uint8_t* rep,
+                     const uint16_t* rep_size, const uint16_t* rep_len, const uint8_t* rep_mask,
+                     const uint32_t* sid_base, const uint32_t* rid_base, or_decode_status* st,
+                     int use_simd, int nthreads);
+
+/* ----------------------------------------------------- streaming protocol (packet level) ---- */
+typedef struct or_encoder or_encoder;
+typedef struct or_decoder or_decoder;
+
+/* Packets are delivered to `emit(ctx, bytes, len)` as whole wire packets. */
+typedef void (*or_emit_fn)(void* ctx, const uint8_t* bytes, size_t len);
+/* Decoded / received sources are delivered to `deliver(ctx, id, bytes, len)`. */
+typedef void (*or_deliver_fn)(void* ctx, uint32_t id, const uint8_t* bytes, size_t len);
+
+or_encoder* or_encoder_new(or_emit_fn emit, void* ctx);
+void        or_encoder_free(or_encoder*);
+void        or_encoder_set_rate(or_encoder*, size_t rate);
+void        or_encoder_set_window_size(or_encoder*, size_t sz);
+void        or_encoder_set_code_type(or_encoder*, int systematic);
+void        or_encoder_set_adaptive(or_encoder*, int adaptive);
+void        or_encoder_add_data(or_encoder*, const uint8_t* data, uint16_t len);
+long        or_encoder_add_packet(or_encoder*, const uint8_t* pkt, size_t len); /* -1: type err */
+void        or_encoder_generate_repair(or_encoder*);
+size_t      or_encoder_window(const or_encoder*);
+size_t      or_encoder_rate(const or_encoder*);
+size_t      or_encoder_nb_sent_repairs(const or_encoder*);
+size_t      or_encoder_nb_sent_sources(const or_encoder*);
+size_t      or_encoder_nb_received_acks(const or_encoder*);
+
+or_decoder* or_decoder_new(int in_order, or_emit_fn emit, void* ectx, or_deliver_fn deliver,
+                           void* dctx);
+void        or_decoder_free(or_decoder*);
+long        or_decoder_add_packet(or_decoder*, const uint8_t* pkt, size_t len); /* -1: err */
+void        or_decoder_generate_ack(or_decoder*);
+void        or_decoder_set_ack_nb_packets(or_decoder*, uint16_t nb);
+void        or_decoder_set_ack_period_ms(or_decoder*, long ms);  /* 0 disables timed acks */
+size_t      or_decoder_counter(const or_decoder*, int which);
+/* which: 0 nb_decoded, 1 nb_failed_full_decodings, 2 nb_missing_sources, 3 nb_received_repairs,
+ *        4 nb_received_sources, 5 nb_sent_acks, 6 nb_useless_repairs, 7 nb_repairs_pending */
+
+/* tests/end_to_end.cc:90-201 restated: 1024-B payloads, GF(256), rate 5, in-order decoder, ack
+ * every 50 received packets, loss::burst{95,5} (tools/loss/burst.hh) shared by both directions.
+ * out[0..6] = sent, lost(to decoder), received repairs, received sources, useless, decoded,
+ * handled data.  Returns 0 on success, -1 if the in-order data check fails. */
+int or_end_to_end(uint32_t nb_packets, uint64_t* out);
+
+/* loss models: libstdc++ std::default_random_engine (minstd_rand0, seed 1) +
+ * uniform_int_distribution<unsigned>{1,100} (tools/loss/{burst,uniform}.hh). */
+typedef struct { uint32_t state; int bad; unsigned good_th, bad_th; } or_burst;
+void or_burst_init(or_burst*, unsigned good, unsigned bad);
+int  or_burst_next(or_burst*);           /* 1 = lost */
+typedef struct { uint32_t state; unsigned threshold; } or_uniform;
+void or_uniform_init(or_uniform*, unsigned threshold);
+int  or_uniform_next(or_uniform*);       /* 1 = lost */
+
+/* AVX2 split-nibble region MAC: the algorithm class of gf-complete's w=8 default (SPLIT 8,4
+ * with pshufb); used as the CPU baseline.  Falls back to the scalar loop without AVX2. */
+void or_region_muladd_simd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
+int  or_have_avx2(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,269 @@
+"""ctypes binding of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module. It
+restates ahamez/netcode's GF(2^8) path (see ntc_oracle.c for per-function reference citations)
+and is never used by the product package ``netcode_amd``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libntc_oracle.so")
+_lib = None
+
+
+class DecodeStatus(C.Structure):
+    _fields_ = [("state", C.c_uint8), ("nb_failed", C.c_uint8), ("nb_missing", C.c_uint16),
+                ("nb_decoded", C.c_uint16), ("nb_useless", C.c_uint16),
+                ("last_repair", C.c_uint16), ("pad", C.c_uint16)]
+
+
+DECODE_STATUS_DTYPE = np.dtype([("state", "u1"), ("nb_failed", "u1"), ("nb_missing", "<u2"),
+                                ("nb_decoded", "<u2"), ("nb_useless", "<u2"),
+                                ("last_repair", "<u2"), ("pad", "<u2")])
+
+EMIT = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
+DELIVER = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t)
+
+
+def build() -> str:
+    """Compile the oracle (gcc) in place; idempotent."""
+    src = os.path.join(_HERE, "ntc_oracle.c")
+    if (not os.path.exists(_LIB)) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = C.CDLL(_LIB)
+        P = C.c_void_p
+        u8p, u16p, u32p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint16), C.POINTER(C.c_uint32)
+        L.or_gf_mul.restype = C.c_uint8
+        L.or_gf_mul.argtypes = [C.c_uint8, C.c_uint8]
+        L.or_gf_inv.restype = C.c_uint8
+        L.or_gf_inv.argtypes = [C.c_uint8]
+        L.or_coefficient.restype = C.c_uint32
+        L.or_coefficient.argtypes = [C.c_uint32, C.c_uint32]
+        L.or_multiply_size.restype = C.c_uint16
+        L.or_multiply_size.argtypes = [C.c_uint16, C.c_uint32]
+        L.or_region_mul.argtypes = [P, P, C.c_size_t, C.c_uint8]
+        L.or_region_muladd.argtypes = [P, P, C.c_size_t, C.c_uint8]
+        L.or_region_muladd_simd.argtypes = [P, P, C.c_size_t, C.c_uint8]
+        L.or_invert.restype = C.c_long
+        L.or_invert.argtypes = [P, P, C.c_size_t]
+        L.or_encode_generation.argtypes = [C.c_uint32] * 3 + [P, P, C.c_uint32, C.c_uint32,
+                                                              P, P, P]
+        L.or_encode_batch.argtypes = [C.c_uint32] * 4 + [P, P, P, P, P, P, C.c_int, C.c_int]
+        L.or_decode_batch.argtypes = [C.c_uint32] * 4 + [P] * 11 + [C.c_int, C.c_int]
+        L.or_end_to_end.restype = C.c_int
+        L.or_end_to_end.argtypes = [C.c_uint32, P]
+        L.or_encoder_new.restype = P
+        L.or_encoder_new.argtypes = [EMIT, P]
+        L.or_encoder_free.argtypes = [P]
+        L.or_encoder_set_rate.argtypes = [P, C.c_size_t]
+        L.or_encoder_set_window_size.argtypes = [P, C.c_size_t]
+        L.or_encoder_set_code_type.argtypes = [P, C.c_int]
+        L.or_encoder_set_adaptive.argtypes = [P, C.c_int]
+        L.or_encoder_add_data.argtypes = [P, P, C.c_uint16]
+        L.or_encoder_add_packet.restype = C.c_long
+        L.or_encoder_add_packet.argtypes = [P, P, C.c_size_t]
+        L.or_encoder_generate_repair.argtypes = [P]
+        for n in ("window", "rate", "nb_sent_repairs", "nb_sent_sources", "nb_received_acks"):
+            f = getattr(L, "or_encoder_" + n)
+            f.restype = C.c_size_t
+            f.argtypes = [P]
+        L.or_decoder_new.restype = P
+        L.or_decoder_new.argtypes = [C.c_int, EMIT, P, DELIVER, P]
+        L.or_decoder_free.argtypes = [P]
+        L.or_decoder_add_packet.restype = C.c_long
+        L.or_decoder_add_packet.argtypes = [P, P, C.c_size_t]
+        L.or_decoder_generate_ack.argtypes = [P]
+        L.or_decoder_set_ack_nb_packets.argtypes = [P, C.c_uint16]
+        L.or_decoder_set_ack_period_ms.argtypes = [P, C.c_long]
+        L.or_decoder_counter.restype = C.c_size_t
+        L.or_decoder_counter.argtypes = [P, C.c_int]
+        L.or_have_avx2.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+# --------------------------------------------------------------------------- scalar helpers
+def gf_mul(a: int, b: int) -> int:
+    return lib().or_gf_mul(a, b)
+
+
+def gf_inv(a: int) -> int:
+    return lib().or_gf_inv(a)
+
+
+def coefficient(rid: int, sid: int) -> int:
+    return lib().or_coefficient(rid & 0xFFFFFFFF, sid & 0xFFFFFFFF)
+
+
+def multiply_size(size: int, c: int) -> int:
+    return lib().or_multiply_size(size, c)
+
+
+def mul_table() -> np.ndarray:
+    """256x256 product table (0x11D)."""
+    t = np.zeros((256, 256), np.uint8)
+    L = lib()
+    for a in range(256):
+        src = np.arange(256, dtype=np.uint8)
+        L.or_region_mul(_p(src), _p(t[a]), 256, a)
+    return t
+
+
+def invert(mat_colmajor: np.ndarray):
+    """Returns (failure_index or None, inverse col-major u32)."""
+    n = int(round(np.sqrt(mat_colmajor.size)))
+    m = np.ascontiguousarray(mat_colmajor, dtype=np.uint32).copy()
+    inv = np.zeros(n * n, np.uint32)
+    r = lib().or_invert(_p(m), _p(inv), n)
+    return (None if r < 0 else int(r)), inv
+
+
+# --------------------------------------------------------------------------- batch forms
+def encode_batch(src, src_len, k, r, sid_base=None, rid_base=None, simd=False, threads=1):
+    G, kk, stride = src.shape
+    assert kk == k
+    rep = np.zeros((G, r, stride), np.uint8)
+    rep_size = np.zeros((G, r), np.uint16)
+    lib().or_encode_batch(G, k, r, stride, _p(np.ascontiguousarray(src)),
+                          _p(np.ascontiguousarray(src_len, dtype=np.uint16)),
+                          _p(None if sid_base is None else np.ascontiguousarray(sid_base, np.uint32)),
+                          _p(None if rid_base is None else np.ascontiguousarray(rid_base, np.uint32)),
+                          _p(rep), _p(rep_size), int(simd), int(threads))
+    return rep, rep_size
+
+
+def decode_batch(src, src_len, src_mask, rep, rep_size, rep_mask, sid_base=None, rid_base=None,
+                 rep_len=None, threads=1):
+    """Returns (src_out, src_len_out, status[G]) -- inputs are not modified."""
+    G, k, stride = src.shape
+    r = rep.shape[1]
+    s = np.ascontiguousarray(src).copy()
+    sl = np.ascontiguousarray(src_len, dtype=np.uint16).copy()
+    st = np.zeros(G, DECODE_STATUS_DTYPE)
+    lib().or_decode_batch(G, k, r, stride, _p(s), _p(sl),
+                          _p(np.ascontiguousarray(src_mask, np.uint8)),
+                          _p(np.ascontiguousarray(rep)), _p(np.ascontiguousarray(rep_size, np.uint16)),
+                          _p(None if rep_len is None else np.ascontiguousarray(rep_len, np.uint16)),
+                          _p(np.ascontiguousarray(rep_mask, np.uint8)),
+                          _p(None if sid_base is None else np.ascontiguousarray(sid_base, np.uint32)),
+                          _p(None if rid_base is None else np.ascontiguousarray(rid_base, np.uint32)),
+                          _p(st), 0, int(threads))
+    return s, sl, st
+
+
+def end_to_end(nb_packets: int):
+    out = np.zeros(7, np.uint64)
+    rc = lib().or_end_to_end(nb_packets, _p(out))
+    keys = ["sent", "lost", "received_repairs", "received_sources", "useless_repairs", "decoded",
+            "handled_data"]
+    return rc, dict(zip(keys, (int(x) for x in out)))
+
+
+# --------------------------------------------------------------------------- streaming objects
+class Encoder:
+    """Packet-level restatement of ntc::encoder (encoder.hh); packets collected in .packets."""
+
+    def __init__(self):
+        self.packets: list[bytes] = []
+        self._cb = EMIT(lambda ctx, p, n: self.packets.append(C.string_at(p, n)))
+        self.h = lib().or_encoder_new(self._cb, None)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_encoder_free(self.h)
+            self.h = None
+
+    def add_data(self, data: bytes):
+        buf = np.frombuffer(bytes(data), np.uint8).copy() if data else np.zeros(1, np.uint8)
+        lib().or_encoder_add_data(self.h, _p(buf), len(data))
+
+    def add_packet(self, pkt: bytes) -> int:
+        buf = np.frombuffer(bytes(pkt), np.uint8).copy()
+        return lib().or_encoder_add_packet(self.h, _p(buf), len(pkt))
+
+    def generate_repair(self):
+        lib().or_encoder_generate_repair(self.h)
+
+    def set_rate(self, r):
+        lib().or_encoder_set_rate(self.h, r)
+
+    def set_window_size(self, s):
+        lib().or_encoder_set_window_size(self.h, s)
+
+    def set_code_type(self, systematic: bool):
+        lib().or_encoder_set_code_type(self.h, int(systematic))
+
+    def set_adaptive(self, a: bool):
+        lib().or_encoder_set_adaptive(self.h, int(a))
+
+    @property
+    def window(self):
+        return lib().or_encoder_window(self.h)
+
+    @property
+    def rate(self):
+        return lib().or_encoder_rate(self.h)
+
+    @property
+    def nb_sent_repairs(self):
+        return lib().or_encoder_nb_sent_repairs(self.h)
+
+    @property
+    def nb_sent_sources(self):
+        return lib().or_encoder_nb_sent_sources(self.h)
+
+
+class Decoder:
+    """Packet-level restatement of ntc::decoder (decoder.hh); deliveries in .data."""
+
+    COUNTERS = ["nb_decoded", "nb_failed_full_decodings", "nb_missing_sources",
+                "nb_received_repairs", "nb_received_sources", "nb_sent_acks",
+                "nb_useless_repairs", "nb_pending_repairs"]
+
+    def __init__(self, in_order: bool = True):
+        self.packets: list[bytes] = []
+        self.data: list[tuple[int, bytes]] = []
+        self._ecb = EMIT(lambda ctx, p, n: self.packets.append(C.string_at(p, n)))
+        self._dcb = DELIVER(lambda ctx, i, p, n: self.data.append((i, C.string_at(p, n))))
+        self.h = lib().or_decoder_new(int(in_order), self._ecb, None, self._dcb, None)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_decoder_free(self.h)
+            self.h = None
+
+    def add_packet(self, pkt: bytes) -> int:
+        buf = np.frombuffer(bytes(pkt), np.uint8).copy()
+        return lib().or_decoder_add_packet(self.h, _p(buf), len(pkt))
+
+    def generate_ack(self):
+        lib().or_decoder_generate_ack(self.h)
+
+    def set_ack_nb_packets(self, n):
+        lib().or_decoder_set_ack_nb_packets(self.h, n)
+
+    def set_ack_period_ms(self, ms):
+        lib().or_decoder_set_ack_period_ms(self.h, ms)
+
+    def __getattr__(self, name):
+        if name in Decoder.COUNTERS:
+            return lib().or_decoder_counter(self.h, Decoder.COUNTERS.index(name))
+        raise AttributeError(name)

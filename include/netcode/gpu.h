@@ -1,0 +1,120 @@
+/*
+ * netcode/gpu.h -- batched GF(2^8) network-coding engine for MI355X (gfx950).
+ *
+ * C ABI (plain pointers and sizes, no HIP/torch types) behind which the hand-written CDNA4 HIP
+ * kernels of libntc_gf256.so run.  It replaces, for whole batches of independent generations,
+ * the reference's per-packet GF region calls:
+ *
+ *   ntc_gf256_encode_batch   <- ntc::detail::encoder::operator()   netcode/detail/encoder.cc:15-64
+ *                               (galois_field::multiply / multiply_add / multiply_size,
+ *                                netcode/detail/galois_field.hh:65-120), one call per repair in
+ *                               ntc::encoder::generate_repair (netcode/encoder.hh:162-169).
+ *   ntc_gf256_decode_batch   <- ntc::detail::decoder::operator()(decoder_repair&&) and
+ *                               attempt_full_decoding (netcode/detail/decoder.cc:54-152,
+ *                               393-408, 412-566) + detail::invert (invert_matrix.cc:9-128).
+ *   ntc_gf256_region_multiply<- galois_field::multiply / multiply_add (galois_field.hh:65-92).
+ *   ntc_gf256_coefficient    <- galois_field::coefficient (galois_field.hh:143-158, w = 8).
+ *   ntc_gf256_multiply_size  <- galois_field::multiply_size (galois_field.hh:96-120, w = 8).
+ *
+ * Layout contract (all device pointers, caller-owned, HBM-resident):
+ *   src       [G][k][stride] bytes, slot i of generation g holds source id sid_base[g] + i,
+ *             zero-padded after src_len[g][i] bytes (the reference zero-pads shorter sources,
+ *             detail/encoder.cc:44-48).
+ *   rep       [G][r][stride] bytes, slot j holds repair id rid_base[g] + j.
+ *   stride    multiple of 16, >= the longest symbol; symbols are u16-sized (<= 65535 B).
+ *   sid_base / rid_base: [G] u32 or NULL (then g*k and g*r).  Ids must not wrap inside a
+ *             generation (sid_base + k <= 2^32); the coefficient product itself wraps exactly
+ *             like the reference's uint32 arithmetic.
+ * All calls are asynchronous on `stream` (a hipStream_t, NULL = default stream) and return an
+ * ntc_gpu_status; no exceptions cross the ABI.  One engine per device; not thread-safe.
+ */
+#ifndef NETCODE_GPU_H
+#define NETCODE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  NTC_GPU_OK = 0,
+  NTC_GPU_EINVAL = 1,        /* bad argument (sizes, alignment, NULL) */
+  NTC_GPU_ENOMEM = 2,        /* device workspace allocation failed */
+  NTC_GPU_EDEVICE = 3,       /* HIP runtime error (launch / device) */
+  NTC_GPU_EUNSUPPORTED = 4   /* shape outside this build's limits (e.g. r > 64) */
+} ntc_gpu_status;
+
+/* Per-generation decode outcome; the same fields the reference decoder's counters expose
+ * (detail/decoder.cc nb_decoded / nb_failed_full_decodings / nb_useless_repairs) when the
+ * generation's received sources and then its received repairs are fed in ascending id order. */
+typedef struct {
+  uint8_t  state;        /* 0 decoded, 1 nothing missing, 2 not enough repairs, 3 all attempts
+                            singular (every candidate matrix non-invertible) */
+  uint8_t  nb_failed;    /* failed full decodings (singular matrices; detail/decoder.cc:448-468) */
+  uint16_t nb_missing;   /* m = lost sources in the generation */
+  uint16_t nb_decoded;   /* sources recovered */
+  uint16_t nb_useless;   /* repairs dropped as useless (detail/decoder.cc:77-89) */
+  uint16_t last_repair;  /* slot of the repair that completed decoding, 0xFFFF if none */
+  uint16_t pad;
+} ntc_gf256_decode_status;
+
+typedef struct ntc_gf256_engine ntc_gf256_engine;
+
+/* Create an engine bound to HIP device `device`; builds the device-resident coefficient tables. */
+int  ntc_gf256_engine_create(int device, ntc_gf256_engine** out);
+void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
+
+/* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture). */
+int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
+
+/* Encode: rep[g][j] = sum_i c(rid_base[g]+j, sid_base[g]+i) * src[g][i] over GF(2^8)/0x11D.
+ * rep_size[g][j] = encoded size (XOR of bytewise-coded u16 lengths); rep_len[g] = repair symbol
+ * length = max src_len over the generation (may be NULL). */
+int  ntc_gf256_encode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
+                            uint32_t stride, const uint8_t* src, const uint16_t* src_len,
+                            const uint32_t* sid_base, const uint32_t* rid_base, uint8_t* rep,
+                            uint16_t* rep_size, uint16_t* rep_len, void* stream);
+
+/* Decode in place: lost source slots (src_mask == 0) whose generation decodes are overwritten
+ * with the recovered payload (zero-padded to stride) and their src_len set to the decoded size.
+ * status[g] receives the outcome.  Requires r <= 64 (m <= 64). */
+int  ntc_gf256_decode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
+                            uint32_t stride, uint8_t* src, uint16_t* src_len,
+                            const uint8_t* src_mask, const uint8_t* rep, const uint16_t* rep_size,
+                            const uint8_t* rep_mask, const uint32_t* sid_base,
+                            const uint32_t* rid_base, ntc_gf256_decode_status* status,
+                            void* stream);
+
+/* The two halves of ntc_gf256_decode_batch, exposed for profiling: the per-generation plan
+ * (greedy repair selection + device Gauss-Jordan, writes status and decoded sizes) and the
+ * region multiply-accumulate that applies it. */
+int  ntc_gf256_decode_plan(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
+                           uint16_t* src_len, const uint8_t* src_mask, const uint16_t* rep_size,
+                           const uint8_t* rep_mask, const uint32_t* sid_base,
+                           const uint32_t* rid_base, ntc_gf256_decode_status* status,
+                           void* stream);
+int  ntc_gf256_decode_apply(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
+                            uint32_t stride, uint8_t* src, const uint8_t* rep, void* stream);
+
+/* dst = c*src (add = 0) or dst ^= c*src (add = 1) over `len` bytes of device memory. */
+int  ntc_gf256_region_multiply(ntc_gf256_engine* eng, const uint8_t* src, uint8_t* dst,
+                               size_t len, uint8_t c, int add, void* stream);
+
+/* Host-side scalar helpers (no device work). */
+uint32_t ntc_gf256_coefficient(uint32_t repair_id, uint32_t src_id);
+uint16_t ntc_gf256_multiply_size(uint16_t size, uint32_t coeff);
+uint8_t  ntc_gf256_multiply(uint8_t x, uint8_t y);
+uint8_t  ntc_gf256_invert(uint8_t x);
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* ntc_gf256_last_error(void);
+
+/* Build description: "gfx950 ..." (lets callers check the native library really loaded). */
+const char* ntc_gf256_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,49 @@
+"""Build the native pieces in-tree (no JIT cache): libntc_gf256.so for gfx950 via hipcc.
+
+The .so lands next to this file so it travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+TARGETS = {
+    "libntc_gf256.so": ["csrc/ntc_gf256.hip"],
+}
+
+
+def _stale(out: str, srcs: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    deps = srcs + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))]
+    deps.append(os.path.join(ROOT, "include", "netcode", "gpu.h"))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, verbose: bool = True) -> list[str]:
+    built = []
+    for out, srcs in TARGETS.items():
+        out_p = os.path.join(HERE, out)
+        srcs_p = [os.path.join(HERE, s) for s in srcs]
+        if not force and not _stale(out_p, srcs_p):
+            built.append(out_p)
+            continue
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out_p + ".tmp"] + srcs_p
+        if verbose:
+            print("[netcode_amd.build]", " ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        os.replace(out_p + ".tmp", out_p)
+        built.append(out_p)
+    return built
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

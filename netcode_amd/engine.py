@@ -1,0 +1,232 @@
+"""Host-side mirror of netcode's coding interface over the MI355X engine.
+
+Python surface (device tensors in, device tensors out; the GF work runs in libntc_gf256.so):
+
+* :class:`GaloisField`  -- ``ntc::detail::galois_field`` (netcode/detail/galois_field.hh:18-167):
+  ``coefficient``, ``multiply`` / ``multiply_add`` (device regions), ``multiply_size``,
+  scalar ``multiply`` / ``invert``.  w = 8 only in this build.
+* :class:`BatchEncoder` -- ``ntc::detail::encoder`` (netcode/detail/encoder.cc:15-64) applied to
+  G independent generations of k sources -> r repairs each.
+* :class:`BatchDecoder` -- ``ntc::detail::decoder`` (netcode/detail/decoder.cc:54-152, 412-566)
+  applied to G generations whose received sources then received repairs arrive in id order.
+
+Every call enqueues on torch's current HIP stream for the tensors' device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native
+
+STATUS_DTYPE = np.dtype([("state", "u1"), ("nb_failed", "u1"), ("nb_missing", "<u2"),
+                         ("nb_decoded", "<u2"), ("nb_useless", "<u2"),
+                         ("last_repair", "<u2"), ("pad", "<u2")])
+STATUS_BYTES = STATUS_DTYPE.itemsize  # 12
+
+DECODED, NOTHING_MISSING, NOT_ENOUGH_REPAIRS, SINGULAR = 0, 1, 2, 3
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev: torch.device):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _require(t: torch.Tensor, name: str, dtype, shape, dev):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device != dev:
+        raise ValueError(f"{name} must live on {dev}, got {t.device}")
+    if t.dtype not in dtype:
+        raise TypeError(f"{name} must have dtype {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+_U8 = (torch.uint8,)
+_U16 = (torch.int16, torch.uint16)
+_U32 = (torch.int32, torch.uint32)
+
+
+class Engine:
+    """One native engine per HIP device (ntc_gf256_engine_create)."""
+
+    _per_device: dict[int, "Engine"] = {}
+
+    def __init__(self, device: int | torch.device = 0):
+        L = _native.load()
+        dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("the GF(256) engine runs on a HIP device")
+        self.device = torch.device("cuda", dev.index if dev.index is not None else 0)
+        h = _native.C.c_void_p()
+        _native.check(L.ntc_gf256_engine_create(self.device.index, _native.C.byref(h)),
+                      "ntc_gf256_engine_create")
+        self._h = h
+        self._L = L
+
+    @classmethod
+    def get(cls, device: int | torch.device = 0) -> "Engine":
+        idx = device if isinstance(device, int) else (torch.device(device).index or 0)
+        if idx not in cls._per_device:
+            cls._per_device[idx] = Engine(idx)
+        return cls._per_device[idx]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ntc_gf256_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown ordering
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reserve(self, G: int, k: int, r: int):
+        _native.check(self._L.ntc_gf256_reserve(self._h, G, k, r), "ntc_gf256_reserve")
+
+
+class GaloisField:
+    """``ntc::detail::galois_field`` for w = 8 (galois_field.hh:18-167)."""
+
+    def __init__(self, w: int = 8, device: int | torch.device = 0):
+        if w != 8:
+            raise NotImplementedError("this build implements GF(2^8) only (w = 8)")
+        self.w = w
+        self._L = _native.load()
+        self._dev = device
+
+    def size(self) -> int:
+        return self.w
+
+    def coefficient(self, repair_id: int, src_id: int) -> int:
+        return self._L.ntc_gf256_coefficient(repair_id & 0xFFFFFFFF, src_id & 0xFFFFFFFF)
+
+    def multiply_size(self, size: int, coeff: int) -> int:
+        return self._L.ntc_gf256_multiply_size(size, coeff)
+
+    def multiply_scalar(self, x: int, y: int) -> int:
+        return self._L.ntc_gf256_multiply(x, y)
+
+    def invert(self, x: int) -> int:
+        if x == 0:
+            raise ZeroDivisionError("0 has no inverse in GF(2^8)")
+        return self._L.ntc_gf256_invert(x)
+
+    def _region(self, src: torch.Tensor, dst: torch.Tensor, length: int, coeff: int, add: int):
+        if src.dtype != torch.uint8 or dst.dtype != torch.uint8:
+            raise TypeError("regions are uint8 tensors")
+        if not (src.is_cuda and dst.is_cuda) or src.device != dst.device:
+            raise ValueError("regions must be device tensors on the same device")
+        if length > src.numel() or length > dst.numel():
+            raise ValueError("length exceeds region")
+        eng = Engine.get(src.device)
+        _native.check(self._L.ntc_gf256_region_multiply(eng.handle, src.data_ptr(), dst.data_ptr(),
+                                                       length, coeff & 0xFF, add,
+                                                       _stream(src.device)),
+                      "ntc_gf256_region_multiply")
+
+    def multiply(self, src: torch.Tensor, dst: torch.Tensor, length: int, coeff: int):
+        """dst[:length] = coeff * src[:length]  (galois_field.hh:65-75)."""
+        self._region(src, dst, length, coeff, 0)
+
+    def multiply_add(self, src: torch.Tensor, dst: torch.Tensor, length: int, coeff: int):
+        """dst[:length] ^= coeff * src[:length]  (galois_field.hh:83-92)."""
+        self._region(src, dst, length, coeff, 1)
+
+
+@dataclass
+class EncodeResult:
+    repairs: torch.Tensor      # [G, r, stride] uint8
+    encoded_size: torch.Tensor  # [G, r] int16 (u16 bits)
+    symbol_len: torch.Tensor   # [G] int16 (u16 bits): repair symbol length = max source length
+
+
+class BatchEncoder:
+    """G generations x (k sources -> r repairs), reference coefficient schedule."""
+
+    def __init__(self, k: int, r: int, device: int | torch.device = 0):
+        self.k, self.r = int(k), int(r)
+        self.engine = Engine.get(device)
+        self.device = self.engine.device
+
+    def __call__(self, src: torch.Tensor, src_len: torch.Tensor, sid_base: torch.Tensor | None = None,
+                 rid_base: torch.Tensor | None = None, out: EncodeResult | None = None) -> EncodeResult:
+        G, k, stride = src.shape
+        if k != self.k:
+            raise ValueError(f"expected k={self.k}, got {k}")
+        dev = self.device
+        _require(src, "src", _U8, (G, k, stride), dev)
+        _require(src_len, "src_len", _U16, (G, k), dev)
+        if sid_base is not None:
+            _require(sid_base, "sid_base", _U32, (G,), dev)
+        if rid_base is not None:
+            _require(rid_base, "rid_base", _U32, (G,), dev)
+        if out is None:
+            out = EncodeResult(torch.empty((G, self.r, stride), dtype=torch.uint8, device=dev),
+                               torch.empty((G, self.r), dtype=torch.int16, device=dev),
+                               torch.empty((G,), dtype=torch.int16, device=dev))
+        L = _native.load()
+        _native.check(L.ntc_gf256_encode_batch(self.engine.handle, G, k, self.r, stride,
+                                               src.data_ptr(), src_len.data_ptr(), _ptr(sid_base),
+                                               _ptr(rid_base), out.repairs.data_ptr(),
+                                               out.encoded_size.data_ptr(),
+                                               out.symbol_len.data_ptr(), _stream(dev)),
+                      "ntc_gf256_encode_batch")
+        return out
+
+
+class BatchDecoder:
+    """In-place generation decode; returns a [G, 12] uint8 status tensor (see STATUS_DTYPE)."""
+
+    def __init__(self, k: int, r: int, device: int | torch.device = 0):
+        self.k, self.r = int(k), int(r)
+        self.engine = Engine.get(device)
+        self.device = self.engine.device
+
+    def __call__(self, src: torch.Tensor, src_len: torch.Tensor, src_mask: torch.Tensor,
+                 rep: torch.Tensor, rep_size: torch.Tensor, rep_mask: torch.Tensor,
+                 sid_base: torch.Tensor | None = None, rid_base: torch.Tensor | None = None,
+                 status: torch.Tensor | None = None) -> torch.Tensor:
+        G, k, stride = src.shape
+        dev = self.device
+        if k != self.k:
+            raise ValueError(f"expected k={self.k}, got {k}")
+        _require(src, "src", _U8, (G, k, stride), dev)
+        _require(src_len, "src_len", _U16, (G, k), dev)
+        _require(src_mask, "src_mask", _U8, (G, k), dev)
+        _require(rep, "rep", _U8, (G, self.r, stride), dev)
+        _require(rep_size, "rep_size", _U16, (G, self.r), dev)
+        _require(rep_mask, "rep_mask", _U8, (G, self.r), dev)
+        if sid_base is not None:
+            _require(sid_base, "sid_base", _U32, (G,), dev)
+        if rid_base is not None:
+            _require(rid_base, "rid_base", _U32, (G,), dev)
+        if status is None:
+            status = torch.empty((G, STATUS_BYTES), dtype=torch.uint8, device=dev)
+        L = _native.load()
+        _native.check(L.ntc_gf256_decode_batch(self.engine.handle, G, k, self.r, stride,
+                                               src.data_ptr(), src_len.data_ptr(),
+                                               src_mask.data_ptr(), rep.data_ptr(),
+                                               rep_size.data_ptr(), rep_mask.data_ptr(),
+                                               _ptr(sid_base), _ptr(rid_base), status.data_ptr(),
+                                               _stream(dev)),
+                      "ntc_gf256_decode_batch")
+        return status
+
+
+def status_to_numpy(status: torch.Tensor) -> np.ndarray:
+    """[G, 12] uint8 device tensor -> structured numpy array (STATUS_DTYPE)."""
+    return status.cpu().numpy().view(STATUS_DTYPE).reshape(-1)

@@ -63,7 +63,7 @@ def lib():
         L.or_encode_generation.argtypes = [C.c_uint32] * 3 + [P, P, C.c_uint32, C.c_uint32,
                                                               P, P, P]
         L.or_encode_batch.argtypes = [C.c_uint32] * 4 + [P, P, P, P, P, P, C.c_int, C.c_int]
-        L.or_decode_batch.argtypes = [C.c_uint32] * 4 + [P] * 11 + [C.c_int, C.c_int]
+        L.or_decode_batch.argtypes = [C.c_uint32] * 4 + [P] * 10 + [C.c_int, C.c_int]
         L.or_end_to_end.restype = C.c_int
         L.or_end_to_end.argtypes = [C.c_uint32, P]
         L.or_encoder_new.restype = P

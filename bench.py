@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""Device-resident GF(256) encode+decode throughput (BASELINE.json metric) on MI355X.
+
+One step = encode G generations (k sources -> r repairs) + decode the same G generations with
+m lost sources each (received sources + repairs -> recovered sources), all buffers resident in
+HBM.  value = G*k*S payload bytes per step / step time (GiB/s), aggregated over ranks.
+
+Multi-GPU (torchrun): every rank owns G independent generations with its own id range (weak
+scaling, no data-path collective); only a barrier and a max-reduce of the timing use RCCL.
+
+Extras in the JSON line: roofline (dominant kernel, HIP-event timed on the engine's stream),
+cpu_baseline (the oracle's AVX2 split-nibble path on this host, bounded sample), host-resident
+rate (pinned H2D + kernels + D2H), per-kernel times.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (k, r, S, stride, m, G)  -- BASELINE.json configs[1..3]
+    "k32r8s1024": (32, 8, 1024, 1024, 8, 4096),
+    "k128r32s4096": (128, 32, 4096, 4096, 32, 4096),
+    "k128r32s1500": (128, 32, 1500, 1504, 32, 8192),
+}
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes/clk x 2.4 GHz
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="k128r32s4096", choices=sorted(CONFIGS))
+    p.add_argument("--G", type=int, default=0, help="generations per GPU (default per config)")
+    p.add_argument("--mixed", action="store_true", help="m ~ U[0, r] instead of m = r")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-rate", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    return p.parse_args()
+
+
+def loss_mask(G, k, m, mixed, seed):
+    rng = np.random.default_rng(seed)
+    mask = np.ones((G, k), np.uint8)
+    keys = rng.random((G, k)).argsort(axis=1)
+    ms = rng.integers(0, m + 1, size=G) if mixed else np.full(G, m)
+    for mm in np.unique(ms):
+        rows = np.nonzero(ms == mm)[0]
+        if mm:
+            mask[rows[:, None], keys[rows, :mm]] = 0
+    return mask
+
+
+class Workload:
+    def __init__(self, dev, G, k, r, S, stride, m, mixed, rank):
+        from netcode_amd import BatchDecoder, BatchEncoder
+        self.dev, self.G, self.k, self.r, self.S, self.stride, self.m = dev, G, k, r, S, stride, m
+        gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+        self.src = torch.randint(0, 256, (G, k, stride), dtype=torch.uint8, device=dev, generator=gen)
+        if stride != S:
+            self.src[:, :, S:] = 0
+        self.src_len = torch.full((G, k), S, dtype=torch.int16, device=dev)
+        base = rank * G
+        self.sid = ((torch.arange(G, device=dev, dtype=torch.int64) + base) * k).to(torch.int32)
+        self.rid = ((torch.arange(G, device=dev, dtype=torch.int64) + base) * r).to(torch.int32)
+        mask = loss_mask(G, k, m, mixed, 99 + rank)
+        self.nlost = int((mask == 0).sum())
+        self.smask = torch.from_numpy(mask).to(dev)
+        self.rmask = torch.ones((G, r), dtype=torch.uint8, device=dev)
+        self.rx = self.src * self.smask[:, :, None]            # decoder-side slots
+        self.rx_len = self.src_len * self.smask.to(torch.int16)
+        self.enc = BatchEncoder(k, r, dev)
+        self.dec = BatchDecoder(k, r, dev)
+        self.out = None
+        self.status = torch.empty((G, 12), dtype=torch.uint8, device=dev)
+        self.enc.engine.reserve(G, k, r)
+
+    def step(self):
+        self.out = self.enc(self.src, self.src_len, self.sid, self.rid, self.out)
+        self.dec(self.rx, self.rx_len, self.smask, self.out.repairs, self.out.encoded_size,
+                 self.rmask, self.sid, self.rid, self.status)
+
+    def kernel_times(self, reps=5):
+        """Per-kernel HIP-event times (ms) on the stream the engine launches on."""
+        from netcode_amd import _native
+        L = _native.load()
+        s = torch.cuda.current_stream(self.dev)
+        h = self.enc.engine.handle
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        t_enc, t_plan, t_apply = [], [], []
+        for _ in range(reps):
+            ev[0].record(s)
+            self.out = self.enc(self.src, self.src_len, self.sid, self.rid, self.out)
+            ev[1].record(s)
+            _native.check(L.ntc_gf256_decode_plan(
+                h, self.G, self.k, self.r, self.rx_len.data_ptr(), self.smask.data_ptr(),
+                self.out.encoded_size.data_ptr(), self.rmask.data_ptr(), self.sid.data_ptr(),
+                self.rid.data_ptr(), self.status.data_ptr(), s.cuda_stream), "plan")
+            ev[2].record(s)
+            _native.check(L.ntc_gf256_decode_apply(h, self.G, self.k, self.r, self.stride,
+                                                   self.rx.data_ptr(), self.out.repairs.data_ptr(),
+                                                   s.cuda_stream), "apply")
+            ev[3].record(s)
+            torch.cuda.synchronize(self.dev)
+            t_enc.append(ev[0].elapsed_time(ev[1]))
+            t_plan.append(ev[1].elapsed_time(ev[2]))
+            t_apply.append(ev[2].elapsed_time(ev[3]))
+        return float(np.mean(t_enc)), float(np.mean(t_plan)), float(np.mean(t_apply))
+
+    def verify(self):
+        from netcode_amd import status_to_numpy
+        st = status_to_numpy(self.status)
+        ok = torch.from_numpy(st["state"] == 0).to(self.dev)
+        good = bool((self.rx[ok] == self.src[ok]).all())
+        return good, int(ok.sum().item())
+
+
+def host_rate(w, reps=3):
+    """Pinned host -> device -> host round trip for the same step (PCIe-inclusive GiB/s)."""
+    dev = w.dev
+    h_src = torch.empty_like(w.src, device="cpu").pin_memory()
+    h_src.copy_(w.src)
+    h_rx = torch.empty_like(w.rx, device="cpu").pin_memory()
+    h_rx.copy_(w.rx)
+    h_rep = torch.empty((w.G, w.r, w.stride), dtype=torch.uint8).pin_memory()
+    d_src = torch.empty_like(w.src)
+    d_rx = torch.empty_like(w.rx)
+    torch.cuda.synchronize(dev)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        d_src.copy_(h_src, non_blocking=True)
+        out = w.enc(d_src, w.src_len, w.sid, w.rid, w.out)
+        h_rep.copy_(out.repairs, non_blocking=True)
+        d_rx.copy_(h_rx, non_blocking=True)
+        w.dec(d_rx, w.rx_len, w.smask, out.repairs, out.encoded_size, w.rmask, w.sid, w.rid,
+              w.status)
+        h_rx.copy_(d_rx, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    return w.G * w.k * w.S / min(times) / 2**30
+
+
+def cpu_baseline(k, r, S, stride, m, threads, budget_s=12.0):
+    """Oracle's AVX2 split-nibble path (gf-complete's w=8 algorithm class), same workload shape,
+    bounded sample; returns dict for the JSON line."""
+    from oracle import oracle as O
+    L = O.lib()
+    L.or_set_simd(1)
+    try:
+        G = 8
+        rng = np.random.default_rng(7)
+        src = rng.integers(0, 256, (G, k, stride), dtype=np.uint8)
+        src[:, :, S:] = 0
+        lens = np.full((G, k), S, np.uint16)
+        mask = loss_mask(G, k, m, False, 8)
+        rmask = np.ones((G, r), np.uint8)
+        # calibrate on one generation (single thread), then size the sample to the budget
+        t0 = time.perf_counter()
+        rep, rsz = O.encode_batch(src[:1], lens[:1], k, r, simd=True, threads=1)
+        lost = src[:1] * mask[:1, :, None]
+        O.decode_batch(lost, lens[:1] * mask[:1], mask[:1], rep, rsz, rmask[:1])
+        per_gen = time.perf_counter() - t0
+        Gs = int(max(threads, min(4096, budget_s / max(per_gen, 1e-6) * threads / 2)))
+        Gs = max(threads, (Gs // threads) * threads)
+        src = np.ascontiguousarray(np.broadcast_to(src[:1], (Gs, k, stride)))
+        lens = np.full((Gs, k), S, np.uint16)
+        mask = loss_mask(Gs, k, m, False, 9)
+        rmask = np.ones((Gs, r), np.uint8)
+        lost = src * mask[:, :, None]
+        llen = lens * mask
+        t0 = time.perf_counter()
+        rep, rsz = O.encode_batch(src, lens, k, r, simd=True, threads=threads)
+        t1 = time.perf_counter()
+        O.decode_batch(lost, llen, mask, rep, rsz, rmask, threads=threads)
+        t2 = time.perf_counter()
+    finally:
+        L.or_set_simd(0)
+    gib = Gs * k * S / 2**30
+    return {"value": round(gib / (t2 - t0), 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{Gs} generations k={k} r={r} S={S} m={m}, encode+decode, AVX2 "
+                      f"split-nibble oracle path, {threads} threads, {t2 - t0:.1f}s",
+            "encode_s": round(t1 - t0, 3), "decode_s": round(t2 - t1, 3)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    k, r, S, stride, m, Gdef = CONFIGS[a.config]
+    G = a.G or Gdef
+
+    import __graft_entry__
+    __graft_entry__.build()
+    w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
+
+    for _ in range(a.warmup):
+        w.step()
+    torch.cuda.synchronize(dev)
+    good, ndec = w.verify()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        w.step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    t_enc, t_plan, t_apply = w.kernel_times()
+    ms_step = elapsed / a.steps * 1e3
+    payload = G * k * S * world
+    value = payload / (elapsed / a.steps) / 2**30
+
+    # Roofline of the dominant kernel (algorithmic bytes per launch / HIP-event duration).
+    enc_bytes = G * (k + r) * S                        # read k*S, write r*S per generation
+    m_avg = w.nlost / G
+    dec_bytes = G * (k + m_avg) * S                    # read (k-m)*S + m*S, write m*S
+    if t_enc >= t_apply:
+        dom, t_dom, bytes_dom, macs = "encode_mac", t_enc, enc_bytes, G * r * k * S
+    else:
+        dom, t_dom, bytes_dom, macs = "decode_mac", t_apply, dec_bytes, G * m_avg * k * S
+    achieved = bytes_dom / (t_dom * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            traffic = tj.get(a.config, {}).get(dom)
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": dom,
+            "kernel_ms": round(t_dom, 4), "algorithmic_bytes_per_launch": int(bytes_dom),
+            "byte_macs_per_launch": int(macs),
+            "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2)}
+
+    line = {"metric": "device-resident GF(256) encode+decode GiB/s, k=128 r=32, 4 KiB pkts, 1/2/4/8 GPU",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8 (GF(2^8))",
+            "data": "synthetic (seeded random payloads, exact-m uniform loss)",
+            "config": {"workload": a.config, "k": k, "r": r, "S": S, "stride": stride,
+                       "m": ("U[0,%d]" % m) if a.mixed else m, "generations_per_gpu": G,
+                       "parallelism": f"generation-shard x{world} (no collectives)"},
+            "roofline": roof,
+            "kernels_ms": {"encode_mac": round(t_enc, 4), "decode_plan": round(t_plan, 4),
+                           "decode_mac": round(t_apply, 4)},
+            "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}
+    if rank == 0 and world == 1 and not a.no_host_rate:
+        line["host_resident_GiBps"] = round(host_rate(w), 3)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(k, r, S, stride, m, thr)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    if not good:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

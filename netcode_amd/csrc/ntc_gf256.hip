@@ -21,6 +21,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -139,44 +140,41 @@ __device__ __forceinline__ uint16_t mul_size(uint16_t size, uint8_t c)
 }
 
 struct MacArgs {
-  uint32_t G, k, rows, stride;
+  uint32_t G, k, stride;
+  uint32_t rows;               // encode: r; decode: r (the plan holds m <= r rows per generation)
   uint32_t nrowchunks, ncolchunks;
-  const uint8_t* src;        // [G][k][stride]
-  const uint16_t* src_len;   // [G][k]
-  uint8_t* out;              // encode: rep [G][rows][stride]; decode: src (in place)
-  const uint8_t* rep;        // decode inputs
-  const uint32_t* sid_base;
-  const uint32_t* rid_base;
-  uint16_t* rep_size;        // encode
-  uint16_t* rep_len;         // encode
-  // decode plan
-  const uint16_t* plan_m;    // [G]
-  const uint16_t* plan_in;   // [G][k]
-  const uint16_t* plan_out;  // [G][RP]
-  const uint8_t* plan_coef;  // [G][k][RP]
+  const uint8_t* in0;          // [G][k][stride] sources (encode input / decode received slots)
+  const uint8_t* in1;          // decode: repairs [G][rows][stride]
+  uint8_t* out;                // encode: repairs [G][rows][stride]; decode: source slots (in place)
+  const uint16_t* rows_per_gen;  // decode: plan_m [G]
+  const uint16_t* in_idx;      // decode: plan_in [G][k] (< k: source slot, >= k: repair slot + k)
+  const uint16_t* out_idx;     // decode: plan_out [G][rp] (destination source slot per row)
+  const uint8_t* coef;         // [G][k][rp] coefficient bytes, row-minor
   uint32_t rp;
 };
 
-// ------------------------------------------------------------------------------- encode ----
-template <int R, int D>
-__global__ __launch_bounds__(256) void encode_mac(MacArgs a)
+// One wave computes R output rows x (64 lanes x 4D bytes) of one generation:
+//   out[row] = sum_i coef[i][row] * in[i]
+// Inputs are consumed in pairs with the next pair's loads in flight (register double buffer).
+template <int R, int D, bool DEC>
+__device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t row0, uint32_t nrows,
+                                         uint32_t col, bool active)
 {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t task = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
-  const uint32_t cc = task % a.ncolchunks;
-  task /= a.ncolchunks;
-  const uint32_t rc = task % a.nrowchunks;
-  const uint32_t g = task / a.nrowchunks;
-  if (g >= a.G) return;
-
-  const uint32_t col = cc * (256u * D) + lane * (4u * D);
-  const bool active = col < a.stride;
-  const uint32_t row0 = rc * R;
-  const uint32_t nrows = min(static_cast<uint32_t>(R), a.rows - row0);
-  const uint32_t sidb = a.sid_base ? uniform(a.sid_base[g]) : g * a.k;
-  const uint32_t ridb = (a.rid_base ? uniform(a.rid_base[g]) : g * a.rows) + row0;
   const size_t stride = a.stride;
-  const uint8_t* src = a.src + static_cast<size_t>(g) * a.k * stride + (active ? col : 0);
+  const uint32_t k = a.k;
+  const uint32_t colx = active ? col : 0u;
+  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride + colx;
+  const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride + colx : nullptr;
+  const uint16_t* in = DEC ? a.in_idx + static_cast<size_t>(g) * k : nullptr;
+  const uint8_t* coef = a.coef + static_cast<size_t>(g) * k * a.rp + row0;
+  auto rowptr = [&](uint32_t i) -> const uint8_t* {
+    if constexpr (DEC) {
+      const uint32_t ii = uniform(in[i]);
+      return ii < k ? base0 + ii * stride : base1 + (ii - k) * stride;
+    } else {
+      return base0 + i * stride;
+    }
+  };
 
   uint32_t acc[R][D];
 #pragma unroll
@@ -184,104 +182,20 @@ __global__ __launch_bounds__(256) void encode_mac(MacArgs a)
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[j][d] = 0;
 
-  uint32_t x0[D], x1[D];
-  uint32_t i = 0;
-  for (; i + 1 < a.k; i += 2) {
-    load_row<D>(src + i * stride, x0);
-    load_row<D>(src + (i + 1) * stride, x1);
-    Sel<D> s0, s1;
-    s0.make(x0);
-    s1.make(x1);
-    const uint32_t S0 = sidb + i + 1u;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      if (static_cast<uint32_t>(j) < nrows) {
-        const uint32_t Rr = ridb + j + 1u;
-        const uint32_t c0 = ((Rr + S0) * Rr) % 255u + 1u;
-        const uint32_t c1 = ((Rr + S0 + 1u) * Rr) % 255u + 1u;
-        mac2<D>(acc[j], c0, s0, c1, s1);
-      }
-    }
+  const uint32_t kk = k & ~1u;
+  uint32_t n0[D], n1[D];
+  if (kk) {
+    load_row<D>(rowptr(0), n0);
+    load_row<D>(rowptr(1), n1);
   }
-  if (i < a.k) {
-    load_row<D>(src + i * stride, x0);
-    Sel<D> s0;
-    s0.make(x0);
-    const uint32_t S0 = sidb + i + 1u;
+  for (uint32_t i = 0; i < kk; i += 2) {
+    uint32_t x0[D], x1[D];
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      if (static_cast<uint32_t>(j) < nrows) {
-        const uint32_t Rr = ridb + j + 1u;
-        mac1<D>(acc[j], ((Rr + S0) * Rr) % 255u + 1u, s0);
-      }
+    for (int d = 0; d < D; ++d) { x0[d] = n0[d]; x1[d] = n1[d]; }
+    if (i + 2 < kk) {
+      load_row<D>(rowptr(i + 2), n0);
+      load_row<D>(rowptr(i + 3), n1);
     }
-  }
-
-  if (active) {
-    uint8_t* out = a.out + (static_cast<size_t>(g) * a.rows + row0) * stride + col;
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-      if (static_cast<uint32_t>(j) < nrows) store_row<D>(out + j * stride, acc[j]);
-  }
-
-  // Encoded sizes (detail/encoder.cc:38, 61-62) and repair symbol length, once per row chunk.
-  if (cc == 0) {
-    const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
-    if (lane < nrows) {
-      const uint32_t Rr = ridb + lane + 1u;
-      uint16_t esz = 0;
-      for (uint32_t t = 0; t < a.k; ++t) {
-        const uint32_t c = ((Rr + sidb + t + 1u) * Rr) % 255u + 1u;
-        esz ^= mul_size(len[t], static_cast<uint8_t>(c));
-      }
-      a.rep_size[static_cast<size_t>(g) * a.rows + row0 + lane] = esz;
-    }
-    if (rc == 0 && a.rep_len) {
-      uint32_t mx = 0;
-      for (uint32_t t = lane; t < a.k; t += 64) mx = max(mx, static_cast<uint32_t>(len[t]));
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, o)));
-      if (lane == 0) a.rep_len[g] = static_cast<uint16_t>(mx);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------- decode ----
-template <int R, int D>
-__global__ __launch_bounds__(256) void decode_mac(MacArgs a)
-{
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t task = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
-  const uint32_t cc = task % a.ncolchunks;
-  task /= a.ncolchunks;
-  const uint32_t rc = task % a.nrowchunks;
-  const uint32_t g = task / a.nrowchunks;
-  if (g >= a.G) return;
-  const uint32_t m = uniform(a.plan_m[g]);
-  const uint32_t row0 = rc * R;
-  if (row0 >= m) return;
-  const uint32_t nrows = min(static_cast<uint32_t>(R), m - row0);
-
-  const uint32_t col = cc * (256u * D) + lane * (4u * D);
-  const bool active = col < a.stride;
-  const size_t stride = a.stride;
-  const uint8_t* src = a.src + static_cast<size_t>(g) * a.k * stride + (active ? col : 0);
-  const uint8_t* rep = a.rep + static_cast<size_t>(g) * a.rows * stride + (active ? col : 0);
-  const uint16_t* in = a.plan_in + static_cast<size_t>(g) * a.k;
-  const uint8_t* coef = a.plan_coef + static_cast<size_t>(g) * a.k * a.rp + row0;
-
-  uint32_t acc[R][D];
-#pragma unroll
-  for (int j = 0; j < R; ++j)
-#pragma unroll
-    for (int d = 0; d < D; ++d) acc[j][d] = 0;
-
-  uint32_t x0[D], x1[D];
-  uint32_t i = 0;
-  for (; i + 1 < a.k; i += 2) {
-    const uint32_t i0 = uniform(in[i]), i1 = uniform(in[i + 1]);
-    load_row<D>(i0 < a.k ? src + i0 * stride : rep + (i0 - a.k) * stride, x0);
-    load_row<D>(i1 < a.k ? src + i1 * stride : rep + (i1 - a.k) * stride, x1);
     Sel<D> s0, s1;
     s0.make(x0);
     s1.make(x1);
@@ -289,30 +203,104 @@ __global__ __launch_bounds__(256) void decode_mac(MacArgs a)
     const uint32_t* cw1 = reinterpret_cast<const uint32_t*>(coef + (i + 1) * a.rp);
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      if (static_cast<uint32_t>(j) < nrows) {
-        const uint32_t c0 = (cw0[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-        const uint32_t c1 = (cw1[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-        mac2<D>(acc[j], c0, s0, c1, s1);
-      }
+      const uint32_t c0 = (cw0[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      const uint32_t c1 = (cw1[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      mac2<D>(acc[j], c0, s0, c1, s1);
     }
   }
-  if (i < a.k) {
-    const uint32_t i0 = uniform(in[i]);
-    load_row<D>(i0 < a.k ? src + i0 * stride : rep + (i0 - a.k) * stride, x0);
+  if (k & 1u) {
+    uint32_t x0[D];
+    load_row<D>(rowptr(kk), x0);
     Sel<D> s0;
     s0.make(x0);
-    const uint32_t* cw0 = reinterpret_cast<const uint32_t*>(coef + i * a.rp);
+    const uint32_t* cw0 = reinterpret_cast<const uint32_t*>(coef + kk * a.rp);
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-      if (static_cast<uint32_t>(j) < nrows) mac1<D>(acc[j], (cw0[j >> 2] >> (8 * (j & 3))) & 0xFFu, s0);
+    for (int j = 0; j < R; ++j) mac1<D>(acc[j], (cw0[j >> 2] >> (8 * (j & 3))) & 0xFFu, s0);
   }
 
-  if (active) {
-    const uint16_t* outs = a.plan_out + static_cast<size_t>(g) * a.rp + row0;
-    uint8_t* base = a.out + static_cast<size_t>(g) * a.k * stride + col;
+  if (!active) return;
+  if constexpr (DEC) {
+    const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
+    uint8_t* base = a.out + static_cast<size_t>(g) * k * stride + col;
 #pragma unroll
     for (int j = 0; j < R; ++j)
       if (static_cast<uint32_t>(j) < nrows) store_row<D>(base + uniform(outs[j]) * stride, acc[j]);
+  } else {
+    uint8_t* base = a.out + (static_cast<size_t>(g) * a.rows + row0) * stride + col;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (static_cast<uint32_t>(j) < nrows) store_row<D>(base + j * stride, acc[j]);
+  }
+}
+
+// Encode (DEC = false): rep[g][rows] = C_g * src[g]; decode (DEC = true): the plan's D_g applied to
+// [repairs ; received sources], written into the lost source slots.  Each wave picks the
+// smallest row tile covering its rows (wave-uniform branch), so no per-row guards in the loop.
+template <int D, bool DEC>
+__global__ __launch_bounds__(256) void gf_mac(MacArgs a)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t task = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const uint32_t cc = task % a.ncolchunks;
+  task /= a.ncolchunks;
+  const uint32_t rc = task % a.nrowchunks;
+  const uint32_t g = task / a.nrowchunks;
+  if (g >= a.G) return;
+  const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
+  const uint32_t row0 = rc * 32u;
+  if (row0 >= total) return;
+  const uint32_t nrows = min(32u, total - row0);
+  const uint32_t col = cc * (256u * D) + lane * (4u * D);
+  const bool active = col < a.stride;
+  if (nrows > 16) mac_tile<32, D, DEC>(a, g, row0, nrows, col, active);
+  else if (nrows > 8) mac_tile<16, D, DEC>(a, g, row0, nrows, col, active);
+  else if (nrows > 4) mac_tile<8, D, DEC>(a, g, row0, nrows, col, active);
+  else mac_tile<4, D, DEC>(a, g, row0, nrows, col, active);
+}
+
+// Encode preparation, one block per generation: the reference coefficient matrix
+// (galois_field.hh:143-158, uint32 wraparound) as [k][rp] bytes, the encoded sizes
+// (detail/encoder.cc:38, 61-62: XOR of bytewise-coded u16 lengths) and the repair symbol length
+// (max source length, detail/encoder.cc:26, 44-48).
+struct PrepArgs {
+  uint32_t G, k, r, rp;
+  const uint16_t* src_len;
+  const uint32_t* sid_base;
+  const uint32_t* rid_base;
+  uint8_t* coef;
+  uint16_t* rep_size;
+  uint16_t* rep_len;
+};
+
+__global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
+{
+  const uint32_t g = blockIdx.x;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
+  uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp;
+  const uint32_t n = a.k * a.rp;
+  for (uint32_t t = threadIdx.x * 4; t < n; t += 256 * 4) {
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+      const uint32_t i = (t + b) / a.rp, j = (t + b) % a.rp;
+      if (j < a.r) w |= coefficient(ridb + j, sidb + i) << (8 * b);
+    }
+    *reinterpret_cast<uint32_t*>(coef + t) = w;   // rp is a multiple of 4
+  }
+  const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
+  for (uint32_t j = threadIdx.x; j < a.r; j += 256) {
+    uint16_t esz = 0;
+    for (uint32_t i = 0; i < a.k; ++i)
+      esz ^= mul_size(len[i], static_cast<uint8_t>(coefficient(ridb + j, sidb + i)));
+    a.rep_size[static_cast<size_t>(g) * a.r + j] = esz;
+  }
+  if (a.rep_len && threadIdx.x < 64) {
+    uint32_t mx = 0;
+    for (uint32_t t = threadIdx.x; t < a.k; t += 64) mx = max(mx, static_cast<uint32_t>(len[t]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, o)));
+    if (threadIdx.x == 0) a.rep_len[g] = static_cast<uint16_t>(mx);
   }
 }
 
@@ -556,6 +544,8 @@ struct ntc_gf256_engine {
   uint16_t* plan_in = nullptr;
   uint16_t* plan_out = nullptr;
   uint8_t* plan_coef = nullptr;
+  void* enc_coef = nullptr;
+  size_t enc_coef_cap = 0;
   // geometry of the last plan (decode_apply must match)
   uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
 };
@@ -582,6 +572,12 @@ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 // Column width per lane: widest that still fills most lanes of the last column chunk.
 int pick_d(uint32_t stride)
 {
+  // NTC_GF256_FORCE_D=1|2|4 overrides the choice (tuning experiments only).
+  static const int forced = [] {
+    const char* v = std::getenv("NTC_GF256_FORCE_D");
+    return v ? std::atoi(v) : 0;
+  }();
+  if ((forced == 1 || forced == 2 || forced == 4) && stride % (4u * forced) == 0) return forced;
   // Prefer 16 B per lane (dwordx4) unless the last column chunk would leave >10 % of lanes idle.
   for (int D = 4; D >= 2; D /= 2) {
     const uint32_t span = 256u * D;
@@ -593,29 +589,31 @@ int pick_d(uint32_t stride)
 
 typedef void (*mac_fn)(MacArgs);
 
-template <int R, int D>
-mac_fn encode_ptr() { return encode_mac<R, D>; }
-template <int R, int D>
-mac_fn decode_ptr() { return decode_mac<R, D>; }
-
-mac_fn pick_kernel(bool enc, int R, int D)
+mac_fn pick_kernel(bool dec, int D)
 {
-#define NTC_CASE(RR, DD) \
-  if (R == RR && D == DD) return enc ? encode_ptr<RR, DD>() : decode_ptr<RR, DD>();
-  NTC_CASE(4, 1) NTC_CASE(4, 2) NTC_CASE(4, 4)
-  NTC_CASE(8, 1) NTC_CASE(8, 2) NTC_CASE(8, 4)
-  NTC_CASE(16, 1) NTC_CASE(16, 2) NTC_CASE(16, 4)
-  NTC_CASE(32, 1) NTC_CASE(32, 2) NTC_CASE(32, 4)
-#undef NTC_CASE
-  return nullptr;
+  if (dec) return D == 4 ? gf_mac<4, true> : D == 2 ? gf_mac<2, true> : gf_mac<1, true>;
+  return D == 4 ? gf_mac<4, false> : D == 2 ? gf_mac<2, false> : gf_mac<1, false>;
 }
 
-int pick_r(uint32_t rows)
+// Coefficient rows padded to the row tile the MAC kernel reads (4, 8, 16 or a multiple of 32).
+uint32_t tile_rp(uint32_t r)
 {
-  if (rows <= 4) return 4;
-  if (rows <= 8) return 8;
-  if (rows <= 16) return 16;
-  return 32;
+  if (r <= 4) return 4;
+  if (r <= 8) return 8;
+  if (r <= 16) return 16;
+  return round_up(r, 32);
+}
+
+int ensure_buf(void** p, size_t* cap, size_t need, const char* what)
+{
+  if (need <= *cap) return NTC_GPU_OK;
+  (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  int rc = hip_check(hipMalloc(p, need), what);
+  if (rc) return rc;
+  *cap = need;
+  return NTC_GPU_OK;
 }
 
 int ensure_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t rp)
@@ -635,7 +633,7 @@ int ensure_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t rp)
   if ((rc = hip_check(hipMalloc(&e->plan_m, nG * 2), "hipMalloc plan_m"))) return rc;
   if ((rc = hip_check(hipMalloc(&e->plan_in, nG * nk * 2), "hipMalloc plan_in"))) return rc;
   if ((rc = hip_check(hipMalloc(&e->plan_out, nG * nrp * 2), "hipMalloc plan_out"))) return rc;
-  if ((rc = hip_check(hipMalloc(&e->plan_coef, nG * nk * nrp), "hipMalloc plan_coef"))) return rc;
+  if ((rc = hip_check(hipMalloc(&e->plan_coef, nG * nk * nrp + 64), "hipMalloc plan_coef"))) return rc;
   e->plan_cap_G = nG; e->plan_cap_k = nk; e->plan_cap_rp = nrp;
   return NTC_GPU_OK;
 }
@@ -700,13 +698,18 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_in);
   (void)hipFree(e->plan_out);
   (void)hipFree(e->plan_coef);
+  (void)hipFree(e->enc_coef);
   delete e;
 }
 
 int ntc_gf256_reserve(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r)
 {
   if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
-  return ensure_plan(e, G, k, round_up(r < 4 ? 4 : r, 4));
+  (void)hipSetDevice(e->device);
+  const uint32_t rp = tile_rp(r);
+  int rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+  if (rc) return rc;
+  return ensure_plan(e, G, k, rp);
 }
 
 int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -718,20 +721,27 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   int rc = check_shape(G, k, r, stride);
   if (rc) return rc;
   if (r == 0) return NTC_GPU_OK;
-  const int R = pick_r(r);
+  (void)hipSetDevice(e->device);
+  const uint32_t rp = tile_rp(r);
+  rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  PrepArgs p{};
+  p.G = G; p.k = k; p.r = r; p.rp = rp; p.src_len = src_len; p.sid_base = sid_base;
+  p.rid_base = rid_base; p.coef = static_cast<uint8_t*>(e->enc_coef); p.rep_size = rep_size;
+  p.rep_len = rep_len;
+  hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
+  if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
   const int D = pick_d(stride);
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
-  a.nrowchunks = (r + R - 1) / R;
+  a.nrowchunks = (r + 31) / 32;
   a.ncolchunks = (stride + 256u * D - 1) / (256u * D);
-  a.src = src; a.src_len = src_len; a.out = rep; a.sid_base = sid_base; a.rid_base = rid_base;
-  a.rep_size = rep_size; a.rep_len = rep_len;
+  a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
   const uint64_t tasks = static_cast<uint64_t>(G) * a.nrowchunks * a.ncolchunks;
   const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
-  mac_fn fn = pick_kernel(true, R, D);
-  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(pick_kernel(false, D), dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, st, a);
   return hip_check(hipGetLastError(), "encode_mac launch");
 }
 
@@ -745,7 +755,8 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
   if (G == 0 || k == 0) return fail(NTC_GPU_EINVAL, "G and k must be > 0");
   if (r > static_cast<uint32_t>(kMaxPlanRows)) return fail(NTC_GPU_EUNSUPPORTED, "r > 64 not supported by decode");
   if (k > 65535) return fail(NTC_GPU_EUNSUPPORTED, "k > 65535");
-  const uint32_t rp = round_up(r < 4 ? 4 : r, 4);
+  const uint32_t rp = tile_rp(r);
+  (void)hipSetDevice(e->device);
   int rc = ensure_plan(e, G, k, rp);
   if (rc) return rc;
   PlanArgs p{};
@@ -767,20 +778,18 @@ int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   if (G != e->last_G || k != e->last_k || r != e->last_r)
     return fail(NTC_GPU_EINVAL, "decode_apply geometry differs from the last decode_plan");
   if (r == 0) return NTC_GPU_OK;
-  const int R = pick_r(r);
   const int D = pick_d(stride);
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
-  a.nrowchunks = (r + R - 1) / R;
+  a.nrowchunks = (r + 31) / 32;
   a.ncolchunks = (stride + 256u * D - 1) / (256u * D);
-  a.src = src; a.out = src; a.rep = rep;
-  a.plan_m = e->plan_m; a.plan_in = e->plan_in; a.plan_out = e->plan_out;
-  a.plan_coef = e->plan_coef; a.rp = e->last_rp;
+  a.in0 = src; a.in1 = rep; a.out = src;
+  a.rows_per_gen = e->plan_m; a.in_idx = e->plan_in; a.out_idx = e->plan_out;
+  a.coef = e->plan_coef; a.rp = e->last_rp;
   const uint64_t tasks = static_cast<uint64_t>(G) * a.nrowchunks * a.ncolchunks;
   const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
-  mac_fn fn = pick_kernel(false, R, D);
-  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+  hipLaunchKernelGGL(pick_kernel(true, D), dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), a);
   return hip_check(hipGetLastError(), "decode_mac launch");
 }

@@ -57,10 +57,16 @@ uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id)
   return res % 255u + 1u;
 }
 
+static int g_simd = 0;   /* CPU-baseline mode: route region ops through the AVX2 kernel */
+static void muladd_dispatch(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
+
+void or_set_simd(int on) { gf_init(); g_simd = on; }
+
 /* galois_field.hh:65-75: multiply_region.w32(..., add = 0) */
 void or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
 {
   gf_init();
+  if (g_simd) { memset(dst, 0, len); muladd_dispatch(src, dst, len, c); return; }
   const uint8_t* row = g_mul[c];
   for (size_t i = 0; i < len; ++i) dst[i] = row[src[i]];
 }
@@ -69,6 +75,7 @@ void or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
 void or_region_muladd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
 {
   gf_init();
+  if (g_simd) { muladd_dispatch(src, dst, len, c); return; }
   const uint8_t* row = g_mul[c];
   for (size_t i = 0; i < len; ++i) dst[i] ^= row[src[i]];
 }
@@ -183,13 +190,19 @@ int or_have_avx2(void) { return __builtin_cpu_supports("avx2"); }
 int or_have_avx2(void) { return 0; }
 #endif
 
-void or_region_muladd_simd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
+static void muladd_dispatch(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
 {
-  gf_init();
 #if defined(__x86_64__)
   if (or_have_avx2()) { muladd_avx2(src, dst, len, c); return; }
 #endif
-  or_region_muladd(src, dst, len, c);
+  const uint8_t* row = g_mul[c];
+  for (size_t i = 0; i < len; ++i) dst[i] ^= row[src[i]];
+}
+
+void or_region_muladd_simd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
+{
+  gf_init();
+  muladd_dispatch(src, dst, len, c);
 }
 
 /* ===================================================== generation encode (batch form) ==== */

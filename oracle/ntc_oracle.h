@@ -128,6 +128,8 @@ int  or_uniform_next(or_uniform*);       /* 1 = lost */
  * with pshufb); used as the CPU baseline.  Falls back to the scalar loop without AVX2. */
 void or_region_muladd_simd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
 int  or_have_avx2(void);
+/* Route the oracle's own region ops through the AVX2 kernel (CPU baseline timing only). */
+void or_set_simd(int on);
 
 #ifdef __cplusplus
 }

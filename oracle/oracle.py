@@ -92,6 +92,7 @@ def lib():
         L.or_decoder_counter.restype = C.c_size_t
         L.or_decoder_counter.argtypes = [P, C.c_int]
         L.or_have_avx2.restype = C.c_int
+        L.or_set_simd.argtypes = [C.c_int]
         _lib = L
     return _lib
 

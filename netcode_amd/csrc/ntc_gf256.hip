@@ -132,6 +132,11 @@ __device__ __forceinline__ uint8_t gmul(uint8_t a, uint8_t b)
   return (a == 0 || b == 0) ? 0 : d_field.exp[d_field.log[a] + d_field.log[b]];
 }
 
+__device__ __forceinline__ uint32_t field_inv_dev(uint32_t x)
+{
+  return d_field.exp[(255 - d_field.log[x]) % 255];
+}
+
 __device__ __forceinline__ uint16_t mul_size(uint16_t size, uint8_t c)
 {
   // netcode/detail/galois_field.hh:108-115: a u16 coded as a 2-byte region.
@@ -153,6 +158,71 @@ struct MacArgs {
   uint32_t rp;
 };
 
+// ---- hand-scheduled scalar loads -------------------------------------------------------------
+// The per-row lookup tables and the coefficient words are wave-uniform; they travel through the
+// scalar cache into SGPRs.  hipcc schedules those loads lazily (load -> s_waitcnt lgkmcnt(0) ->
+// use, one round trip per few rows), so they are issued here by inline asm one row (tables) or
+// one source pair (coefficient words) ahead.  SMEM returns out of order, so every wait is
+// lgkmcnt(0); the "+s" operands tie each consumer to the wait that retires its load.
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct Tab {
+  u32x4 ab;   // {a_lo, a_hi, b_lo, b_hi}
+  uint32_t e;
+};
+
+__device__ __forceinline__ Tab sload_table(uint32_t c)
+{
+  Tab t;
+  asm volatile("s_load_dwordx4 %0, %2, %3\n\ts_load_dword %1, %2, %3 offset:0x10"
+               : "=&s"(t.ab), "=s"(t.e) : "s"(&d_perm.w[0][0]), "s"(c << 5) : "memory");
+  return t;
+}
+
+template <int NW> struct CW;
+template <> struct CW<1> { using T = uint32_t; };
+template <> struct CW<2> { using T = u32x2; };
+template <> struct CW<4> { using T = u32x4; };
+template <> struct CW<8> { using T = u32x8; };
+
+template <int NW>
+__device__ __forceinline__ typename CW<NW>::T sload_words(const uint8_t* p)
+{
+  typename CW<NW>::T v;
+  if constexpr (NW == 1) asm volatile("s_load_dword %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+  else if constexpr (NW == 2) asm volatile("s_load_dwordx2 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+  else if constexpr (NW == 4) asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+  else asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+
+template <int NW>
+__device__ __forceinline__ uint32_t cbyte(const typename CW<NW>::T& w, int j)
+{
+  uint32_t word;
+  if constexpr (NW == 1) word = w;
+  else word = w[j >> 2];
+  return (word >> (8 * (j & 3))) & 0xFFu;
+}
+
+template <int D>
+__device__ __forceinline__ void mac2t(uint32_t (&acc)[D], const Tab& t0, const Sel<D>& s0,
+                                      const Tab& t1, const Sel<D>& s1)
+{
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const uint32_t p = xor3(__builtin_amdgcn_perm(t0.ab[1], t0.ab[0], s0.a[d]),
+                            __builtin_amdgcn_perm(t0.ab[3], t0.ab[2], s0.b[d]),
+                            __builtin_amdgcn_perm(t0.e, t0.e, s0.e[d]));
+    const uint32_t q = xor3(__builtin_amdgcn_perm(t1.ab[1], t1.ab[0], s1.a[d]),
+                            __builtin_amdgcn_perm(t1.ab[3], t1.ab[2], s1.b[d]),
+                            __builtin_amdgcn_perm(t1.e, t1.e, s1.e[d]));
+    acc[d] = xor3(acc[d], p, q);
+  }
+}
+
 // One wave computes R output rows x (64 lanes x 4D bytes) of one generation:
 //   out[row] = sum_i coef[i][row] * in[i]
 // Inputs are consumed in pairs with the next pair's loads in flight (register double buffer).
@@ -160,6 +230,8 @@ template <int R, int D, bool DEC>
 __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t row0, uint32_t nrows,
                                          uint32_t col, bool active)
 {
+  constexpr int NW = R / 4;   // coefficient words per input for this row tile
+  using CWT = typename CW<NW>::T;
   const size_t stride = a.stride;
   const uint32_t k = a.k;
   const uint32_t colx = active ? col : 0u;
@@ -167,6 +239,7 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
   const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride + colx : nullptr;
   const uint16_t* in = DEC ? a.in_idx + static_cast<size_t>(g) * k : nullptr;
   const uint8_t* coef = a.coef + static_cast<size_t>(g) * k * a.rp + row0;
+  const uint32_t rp = a.rp;
   auto rowptr = [&](uint32_t i) -> const uint8_t* {
     if constexpr (DEC) {
       const uint32_t ii = uniform(in[i]);
@@ -183,37 +256,67 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
     for (int d = 0; d < D; ++d) acc[j][d] = 0;
 
   const uint32_t kk = k & ~1u;
-  uint32_t n0[D], n1[D];
   if (kk) {
+    uint32_t n0[D], n1[D];
     load_row<D>(rowptr(0), n0);
     load_row<D>(rowptr(1), n1);
-  }
-  for (uint32_t i = 0; i < kk; i += 2) {
-    uint32_t x0[D], x1[D];
+    CWT w0 = sload_words<NW>(coef);
+    CWT w1 = sload_words<NW>(coef + rp);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(w0), "+s"(w1) :: "memory");
+    Tab t0 = sload_table(cbyte<NW>(w0, 0));
+    Tab t1 = sload_table(cbyte<NW>(w1, 0));
+    for (uint32_t i = 0; i < kk; i += 2) {
+      uint32_t x0[D], x1[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) { x0[d] = n0[d]; x1[d] = n1[d]; }
-    if (i + 2 < kk) {
-      load_row<D>(rowptr(i + 2), n0);
-      load_row<D>(rowptr(i + 3), n1);
-    }
-    Sel<D> s0, s1;
-    s0.make(x0);
-    s1.make(x1);
-    const uint32_t* cw0 = reinterpret_cast<const uint32_t*>(coef + i * a.rp);
-    const uint32_t* cw1 = reinterpret_cast<const uint32_t*>(coef + (i + 1) * a.rp);
+      for (int d = 0; d < D; ++d) { x0[d] = n0[d]; x1[d] = n1[d]; }
+      const bool more = i + 2 < kk;
+      if (more) {
+        load_row<D>(rowptr(i + 2), n0);
+        load_row<D>(rowptr(i + 3), n1);
+      }
+      Sel<D> s0, s1;
+      s0.make(x0);
+      s1.make(x1);
+      CWT nw0 = w0, nw1 = w1;
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const uint32_t c0 = (cw0[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-      const uint32_t c1 = (cw1[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-      mac2<D>(acc[j], c0, s0, c1, s1);
+      for (int j = 0; j < R; ++j) {
+        // retire row j's tables (issued one row earlier); then put row j+1's in flight
+        if (j == R - 1) {
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+s"(t0.ab), "+s"(t0.e), "+s"(t1.ab), "+s"(t1.e), "+s"(nw0), "+s"(nw1) :: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(t0.ab), "+s"(t0.e), "+s"(t1.ab), "+s"(t1.e) :: "memory");
+        }
+        if (j == 0 && more) {
+          nw0 = sload_words<NW>(coef + (i + 2) * rp);
+          nw1 = sload_words<NW>(coef + (i + 3) * rp);
+        }
+        Tab u0, u1;
+        if (j + 1 < R) {
+          u0 = sload_table(cbyte<NW>(w0, j + 1));
+          u1 = sload_table(cbyte<NW>(w1, j + 1));
+        } else if (more) {
+          u0 = sload_table(cbyte<NW>(nw0, 0));
+          u1 = sload_table(cbyte<NW>(nw1, 0));
+        } else {
+          u0 = t0;
+          u1 = t1;
+        }
+        mac2t<D>(acc[j], t0, s0, t1, s1);
+        t0 = u0;
+        t1 = u1;
+      }
+      w0 = nw0;
+      w1 = nw1;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   if (k & 1u) {
     uint32_t x0[D];
     load_row<D>(rowptr(kk), x0);
     Sel<D> s0;
     s0.make(x0);
-    const uint32_t* cw0 = reinterpret_cast<const uint32_t*>(coef + kk * a.rp);
+    const uint32_t* cw0 = reinterpret_cast<const uint32_t*>(coef + kk * rp);
 #pragma unroll
     for (int j = 0; j < R; ++j) mac1<D>(acc[j], (cw0[j >> 2] >> (8 * (j & 3))) & 0xFFu, s0);
   }
@@ -328,26 +431,88 @@ struct PlanArgs {
   uint16_t* plan_out;
   uint8_t* plan_coef;
   uint32_t rp;
+  uint32_t ablate;   // tuning only: bit0 skip elimination, bit1 skip D for received sources
 };
+
+// c * x for the four bytes of x with a per-lane coefficient table (v_perm 3/3/2 split).
+__device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
+{
+  return __builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u) ^
+         __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
+         __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
+}
+
+constexpr int kPitchW = (2 * kMaxPlanRows) / 4 + 1;   // dwords per augmented row (odd: no bank conflicts)
+
+// D rows for four received-source positions (one lane): acc[s] holds D[s][p0..p0+3] as bytes.
+template <int R>
+__device__ __forceinline__ void plan_dmac(uint32_t m, uint32_t p0, uint32_t nb, uint32_t sidb,
+                                          const uint16_t* rl, const uint32_t* rq1,
+                                          const uint16_t (*mA)[kMaxPlanRows],
+                                          const uint32_t (*ptab)[8], uint8_t* dst, uint32_t rp)
+{
+  uint32_t S1[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) S1[b] = sidb + rl[p0 + (static_cast<uint32_t>(b) < nb ? b : 0)] + 1u;
+  uint32_t acc[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) acc[t] = 0;
+  for (uint32_t q = 0; q < m; ++q) {
+    const uint32_t R1 = rq1[q];
+    uint32_t x = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) x |= ((((R1 + S1[b]) * R1) % 255u) + 1u) << (8 * b);
+    const uint32_t sa = x & 0x07070707u, sb = (x >> 3) & 0x07070707u, se = (x >> 6) & 0x03030303u;
+    const uint16_t* row = mA[q];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const uint32_t* tb = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(ptab) + row[t]);
+      const uint4 ab = *reinterpret_cast<const uint4*>(tb);
+      const uint32_t e = tb[4];
+      acc[t] ^= xor3(__builtin_amdgcn_perm(ab.y, ab.x, sa), __builtin_amdgcn_perm(ab.w, ab.z, sb),
+                     __builtin_amdgcn_perm(e, e, se));
+    }
+  }
+  for (uint32_t b = 0; b < nb; ++b) {
+    uint8_t* d = dst + b * rp;
+#pragma unroll
+    for (int t = 0; t < R; t += 4) {
+      const uint32_t w = ((acc[t] >> (8 * b)) & 0xFFu) | (((acc[t + 1] >> (8 * b)) & 0xFFu) << 8) |
+                         (((acc[t + 2] >> (8 * b)) & 0xFFu) << 16) | (((acc[t + 3] >> (8 * b)) & 0xFFu) << 24);
+      if (static_cast<uint32_t>(t) < rp) *reinterpret_cast<uint32_t*>(d + t) = w;
+    }
+    for (uint32_t t = R; t < rp; t += 4) *reinterpret_cast<uint32_t*>(d + t) = 0;
+  }
+  (void)m;
+}
 
 __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
 {
   __shared__ uint8_t exp_t[512];
   __shared__ uint8_t log_t[256];
-  __shared__ uint8_t A[kMaxPlanRows][2 * kMaxPlanRows + 4];
+  __shared__ uint32_t A[kMaxPlanRows][kPitchW];       // augmented [M | I], row q = repair q
   __shared__ uint16_t miss[kMaxPlanRows];
   __shared__ uint16_t recv[kMaxPlanRows];
   __shared__ uint16_t reps[kMaxPlanRows];
-  __shared__ uint32_t sizes[kMaxPlanRows];
-  __shared__ uint8_t dacc[64][kMaxPlanRows + 4];
+  __shared__ uint16_t mA[kMaxPlanRows][kMaxPlanRows];   // 32 * (M^-1)[s][q], [q][s]
+  __shared__ uint32_t rq1[kMaxPlanRows];
+  __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
+  __shared__ uint16_t rl[1024];
+  __shared__ uint16_t sl[1024];
+  __shared__ uint16_t rszL[kMaxPlanRows];
+  __shared__ uint32_t szs[kMaxPlanRows];
 
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x;
   for (uint32_t t = lane; t < 512; t += 64) exp_t[t] = d_field.exp[t];
   for (uint32_t t = lane; t < 256; t += 64) log_t[t] = d_field.log[t];
-  __syncthreads();
-  auto mul = [&](uint32_t x, uint32_t y) -> uint32_t {
-    return (x == 0 || y == 0) ? 0u : exp_t[log_t[x] + log_t[y]];
+  for (uint32_t t = lane; t < 256 * 8; t += 64) ptab[t / 8][t % 8] = d_perm.w[t / 8][t % 8];
+  // galois_field::multiply_size (galois_field.hh:108-115) on the LDS tables
+  auto msize = [&](uint32_t size, uint32_t c) -> uint32_t {
+    if (size == 0 || c == 0) return 0u;
+    const uint32_t lc = log_t[c];
+    const uint32_t lo = size & 0xFFu, hi = size >> 8;
+    return (lo ? exp_t[log_t[lo] + lc] : 0u) | ((hi ? exp_t[log_t[hi] + lc] : 0u) << 8);
   };
 
   const uint32_t k = a.k, r = a.r;
@@ -368,6 +533,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
     }
     m += __popcll(b);
   }
+  if (lane < r) rszL[lane] = a.rep_size[static_cast<size_t>(g) * r + lane];
   uint32_t nrecv = 0;
   for (uint32_t base = 0; base < r; base += 64) {
     const uint32_t idx = base + lane;
@@ -384,7 +550,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   ntc_gf256_decode_status st{};
   st.nb_missing = static_cast<uint16_t>(m);
   st.last_repair = 0xFFFF;
-  uint32_t mm = 0;  // rows of the decode matrix written to the plan
+  uint32_t mm = 0;
 
   if (m == 0) {
     st.state = 1;
@@ -392,46 +558,57 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   } else if (nrecv < m || m > kMaxPlanRows) {
     st.state = 2;
   } else {
+    const uint32_t nw = (2 * m + 3) / 4;   // dwords per augmented row in use
     bool ok = false;
     uint32_t t = m - 1;
     for (; t < nrecv; ++t) {
-      for (uint32_t q = lane; q < m; q += 64) reps[q] = (q + 1 < m) ? recv[q] : recv[t];
-      __syncthreads();
-      // A[q][c]: storage row q = repair q (the reference's column-major square_matrix), columns
-      // 0..m-1 = coefficient of missing source c, m..2m-1 = identity.
-      for (uint32_t q = 0; q < m; ++q) {
-        const uint32_t rid = ridb + reps[q];
-        for (uint32_t c = lane; c < 2 * m; c += 64) {
-          A[q][c] = (c < m) ? static_cast<uint8_t>(coefficient(rid, sidb + miss[c]))
-                            : static_cast<uint8_t>((c - m) == q ? 1 : 0);
+      // Lane q builds row q: coefficients of the missing sources, then the identity block.
+      if (lane < m) {
+        const uint32_t rq = (lane + 1 < m) ? recv[lane] : recv[t];
+        reps[lane] = static_cast<uint16_t>(rq);
+        const uint32_t rid = ridb + rq;
+        for (uint32_t w = 0; w < nw; ++w) {
+          uint32_t word = 0;
+          for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t c = 4 * w + b;
+            uint32_t v = 0;
+            if (c < m) v = coefficient(rid, sidb + miss[c]);
+            else if (c < 2 * m) v = (c - m == lane) ? 1u : 0u;
+            word |= v << (8 * b);
+          }
+          A[lane][w] = word;
         }
       }
       __syncthreads();
       bool singular = false;
       for (uint32_t p = 0; p < m; ++p) {
-        const bool cand = lane >= p && lane < m && A[lane][p] != 0;
-        const uint64_t b = __ballot(cand);
+        const uint32_t pw = p >> 2, ps = 8 * (p & 3);
+        const uint32_t f = (lane < m) ? (A[lane][pw] >> ps) & 0xFFu : 0u;
+        const uint64_t b = __ballot(lane >= p && lane < m && f != 0);
         if (b == 0) { singular = true; break; }
         const uint32_t q = __ffsll(static_cast<unsigned long long>(b)) - 1;
         if (q != p) {
-          for (uint32_t c = lane; c < 2 * m; c += 64) {
-            const uint8_t tmp = A[p][c];
-            A[p][c] = A[q][c];
-            A[q][c] = tmp;
+          for (uint32_t w = lane; w < nw; w += 64) {
+            const uint32_t tmp = A[p][w];
+            A[p][w] = A[q][w];
+            A[q][w] = tmp;
           }
-        }
-        __syncthreads();
-        const uint32_t inv = exp_t[(255 - log_t[A[p][p]]) % 255];
-        for (uint32_t c = lane; c < 2 * m; c += 64) A[p][c] = static_cast<uint8_t>(mul(A[p][c], inv));
-        __syncthreads();
-        for (uint32_t q2 = 0; q2 < m; ++q2) {
-          if (q2 == p) continue;
-          const uint32_t f = A[q2][p];
-          __syncthreads();
-          if (f != 0)
-            for (uint32_t c = lane; c < 2 * m; c += 64) A[q2][c] ^= static_cast<uint8_t>(mul(f, A[p][c]));
           __syncthreads();
         }
+        // normalise row p by 1/pivot (uniform coefficient table)
+        const uint32_t piv = (A[p][pw] >> ps) & 0xFFu;
+        const uint32_t* ti = ptab[exp_t[(255 - log_t[piv]) % 255]];
+        for (uint32_t w = lane; w < nw; w += 64) A[p][w] = mul4(ti, A[p][w]);
+        __syncthreads();
+        // eliminate column p from every other row: lane = row, per-lane table of its factor
+        const uint32_t fa = (lane < m && lane != p && !(a.ablate & 1u)) ? (A[lane][pw] >> ps) & 0xFFu : 0u;
+        if (fa != 0) {
+          uint32_t tf[5];
+#pragma unroll
+          for (int e = 0; e < 5; ++e) tf[e] = ptab[fa][e];
+          for (uint32_t w = 0; w < nw; ++w) A[lane][w] ^= mul4(tf, A[p][w]);
+        }
+        __syncthreads();
       }
       if (!singular) { ok = true; break; }
       __syncthreads();
@@ -448,56 +625,78 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
       st.nb_useless = static_cast<uint16_t>(nrecv - 1 - t);
       st.last_repair = recv[t];
       mm = m;
-      // Input list: positions 0..m-1 = the chosen repairs, m..k-1 = received sources ascending.
       uint16_t* pin = a.plan_in + static_cast<size_t>(g) * k;
       uint8_t* pc = a.plan_coef + static_cast<size_t>(g) * k * a.rp;
       uint16_t* pout = a.plan_out + static_cast<size_t>(g) * a.rp;
-      for (uint32_t s = lane; s < a.rp; s += 64) pout[s] = (s < m) ? miss[s] : 0;
-      for (uint32_t s = lane; s < m; s += 64) sizes[s] = 0;
-      __syncthreads();
-      const uint16_t* rsz = a.rep_size + static_cast<size_t>(g) * r;
       const uint16_t* slen = a.src_len + static_cast<size_t>(g) * k;
+      auto minv = [&](uint32_t s, uint32_t q) -> uint32_t {   // (M^-1)[s][q] = A[s][m + q]
+        const uint32_t c = m + q;
+        return (A[s][c >> 2] >> (8 * (c & 3))) & 0xFFu;
+      };
+      for (uint32_t s = lane; s < a.rp; s += 64) pout[s] = (s < m) ? miss[s] : 0;
+      // Positions 0..m-1: the chosen repairs; D[s][q] = (M^-1)[s][q].  Lane = output row s.
       for (uint32_t q = 0; q < m; ++q) {
         if (lane == 0) pin[q] = static_cast<uint16_t>(k + reps[q]);
-        const uint16_t val = rsz[reps[q]];
-        for (uint32_t s = lane; s < a.rp; s += 64) {
-          const uint32_t dsq = (s < m) ? A[s][m + q] : 0u;   // (M^-1)[s][q]
-          pc[static_cast<size_t>(q) * a.rp + s] = static_cast<uint8_t>(dsq);
-          if (s < m) sizes[s] ^= mul_size(val, static_cast<uint8_t>(dsq));
-        }
+        if (lane < a.rp)
+          pc[static_cast<size_t>(q) * a.rp + lane] = static_cast<uint8_t>(lane < m ? minv(lane, q) : 0u);
+      }
+      if (lane < m) {
+        rq1[lane] = ridb + reps[lane] + 1u;
+        szs[lane] = rszL[reps[lane]];           // becomes the reduced encoded size of repair q
+      }
+      const uint32_t R = m <= 8 ? 8u : m <= 16 ? 16u : m <= 32 ? 32u : 64u;
+      for (uint32_t idx = lane; idx < m * R; idx += 64) {
+        const uint32_t q = idx / R, srow = idx % R;
+        mA[q][srow] = static_cast<uint16_t>(srow < m ? 32u * minv(srow, q) : 0u);
       }
       __syncthreads();
-      // Received sources: D[s][j] = sum_q (M^-1)[s][q] * c(rep_q, j); one source per lane,
-      // the lane's column accumulated in LDS (dacc[lane][s]).
+      // Positions m..k-1: received sources ascending; D[s][j] = sum_q (M^-1)[s][q] * c(rep_q, j),
+      // computed as a small v_perm MAC (lane = 4 consecutive positions, x = their coefficients).
       uint32_t pos_base = m;
-      for (uint32_t base = 0; base < k; base += 64) {
-        const uint32_t j = base + lane;
-        const bool got = j < k && smask[j] != 0;
-        const uint64_t b = __ballot(got);
-        if (got) {
-          const uint32_t pos = pos_base + __popcll(b & lt);
-          pin[pos] = static_cast<uint16_t>(j);
-          const uint16_t val = slen[j];
-          for (uint32_t s = 0; s < m; ++s) dacc[lane][s] = 0;
-          for (uint32_t q = 0; q < m; ++q) {
-            const uint32_t lc = log_t[coefficient(ridb + reps[q], sidb + j)];
-            for (uint32_t s = 0; s < m; ++s) {
-              const uint32_t x = A[s][m + q];
-              if (x) dacc[lane][s] ^= exp_t[log_t[x] + lc];
-            }
+      for (uint32_t cbase = 0; cbase < k; cbase += 1024) {
+        const uint32_t cend = min(k, cbase + 1024);
+        uint32_t cnt = 0;
+        for (uint32_t b2 = cbase; b2 < cend; b2 += 64) {
+          const uint32_t j = b2 + lane;
+          const bool got = j < cend && smask[j] != 0;
+          const uint64_t bb = __ballot(got);
+          if (got) {
+            rl[cnt + __popcll(bb & lt)] = static_cast<uint16_t>(j);
+            sl[cnt + __popcll(bb & lt)] = slen[j];
           }
-          uint8_t* col = pc + static_cast<size_t>(pos) * a.rp;
-          for (uint32_t s = 0; s < a.rp; ++s) {
-            const uint32_t dsj = (s < m) ? dacc[lane][s] : 0u;
-            col[s] = static_cast<uint8_t>(dsj);
-            if (s < m) atomicXor(&sizes[s], static_cast<uint32_t>(mul_size(val, static_cast<uint8_t>(dsj))));
+          cnt += __popcll(bb);
+        }
+        __syncthreads();
+        for (uint32_t t2 = lane; t2 < cnt; t2 += 64) pin[pos_base + t2] = rl[t2];
+        // reduced encoded sizes (detail/decoder.cc:402-404): szs[q] ^= c(q, j) (x) len_j over the
+        // chunk's received sources; lanes split the sources, a wave XOR-reduction per repair.
+        for (uint32_t q = 0; q < m; ++q) {
+          const uint32_t R1 = rq1[q];
+          uint32_t e = 0;
+          for (uint32_t t2 = lane; t2 < cnt; t2 += 64)
+            e ^= msize(sl[t2], ((R1 + sidb + rl[t2] + 1u) * R1) % 255u + 1u);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) e ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(e), o));
+          if (lane == 0) szs[q] ^= e;
+        }
+        if (!(a.ablate & 2u)) {
+          for (uint32_t p0 = 4 * lane; p0 < cnt; p0 += 256) {
+            uint8_t* dst = pc + static_cast<size_t>(pos_base + p0) * a.rp;
+            const uint32_t nb = min(4u, cnt - p0);
+            if (R == 8) plan_dmac<8>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
+            else if (R == 16) plan_dmac<16>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
+            else if (R == 32) plan_dmac<32>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
+            else plan_dmac<64>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
           }
         }
-        pos_base += __popcll(b);
+        pos_base += cnt;
+        __syncthreads();
       }
-      __syncthreads();
-      uint16_t* olen = a.src_len + static_cast<size_t>(g) * k;
-      for (uint32_t s = lane; s < m; s += 64) olen[miss[s]] = static_cast<uint16_t>(sizes[s]);
+      // decoded size of missing source s = sum_q (M^-1)[s][q] (x) reduced size of repair q
+      uint32_t sz = 0;
+      if (lane < m)
+        for (uint32_t q = 0; q < m; ++q) sz ^= msize(szs[q], minv(lane, q));
+      if (lane < m) a.src_len[static_cast<size_t>(g) * k + miss[lane]] = static_cast<uint16_t>(sz);
     }
   }
   if (lane == 0) {
@@ -764,6 +963,11 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
   p.rep_mask = rep_mask; p.sid_base = sid_base; p.rid_base = rid_base; p.status = status;
   p.plan_m = e->plan_m; p.plan_in = e->plan_in; p.plan_out = e->plan_out;
   p.plan_coef = e->plan_coef; p.rp = rp;
+  static const uint32_t ablate = [] {
+    const char* v = std::getenv("NTC_GF256_PLAN_ABLATE");
+    return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
+  }();
+  p.ablate = ablate;
   hipLaunchKernelGGL(decode_plan, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
   return hip_check(hipGetLastError(), "decode_plan launch");

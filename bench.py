@@ -71,9 +71,11 @@ class Workload:
         if stride != S:
             self.src[:, :, S:] = 0
         self.src_len = torch.full((G, k), S, dtype=torch.int16, device=dev)
-        base = rank * G
-        self.sid = ((torch.arange(G, device=dev, dtype=torch.int64) + base) * k).to(torch.int32)
-        self.rid = ((torch.arange(G, device=dev, dtype=torch.int64) + base) * r).to(torch.int32)
+        from netcode_amd.shard import generation_shard
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        sid, rid = generation_shard(rank, world, G, k, r)
+        self.sid = torch.from_numpy(sid.view(np.int32)).to(dev)
+        self.rid = torch.from_numpy(rid.view(np.int32)).to(dev)
         mask = loss_mask(G, k, m, mixed, 99 + rank)
         self.nlost = int((mask == 0).sum())
         self.smask = torch.from_numpy(mask).to(dev)
@@ -172,7 +174,7 @@ def cpu_baseline(k, r, S, stride, m, threads, budget_s=12.0):
         lost = src[:1] * mask[:1, :, None]
         O.decode_batch(lost, lens[:1] * mask[:1], mask[:1], rep, rsz, rmask[:1])
         per_gen = time.perf_counter() - t0
-        Gs = int(max(threads, min(4096, budget_s / max(per_gen, 1e-6) * threads / 2)))
+        Gs = int(max(threads, min(1024, budget_s / max(per_gen, 1e-6) * threads / 4)))
         Gs = max(threads, (Gs // threads) * threads)
         src = np.ascontiguousarray(np.broadcast_to(src[:1], (Gs, k, stride)))
         lens = np.full((Gs, k), S, np.uint16)
@@ -180,19 +182,26 @@ def cpu_baseline(k, r, S, stride, m, threads, budget_s=12.0):
         rmask = np.ones((Gs, r), np.uint8)
         lost = src * mask[:, :, None]
         llen = lens * mask
-        t0 = time.perf_counter()
-        rep, rsz = O.encode_batch(src, lens, k, r, simd=True, threads=threads)
-        t1 = time.perf_counter()
-        O.decode_batch(lost, llen, mask, rep, rsz, rmask, threads=threads)
-        t2 = time.perf_counter()
+        t_enc = t_dec = 0.0
+        passes = 0
+        while passes < 1 or (t_enc + t_dec < budget_s and passes < 64):
+            t0 = time.perf_counter()
+            rep, rsz = O.encode_batch(src, lens, k, r, simd=True, threads=threads)
+            t1 = time.perf_counter()
+            O.decode_batch(lost, llen, mask, rep, rsz, rmask, threads=threads)
+            t2 = time.perf_counter()
+            t_enc += t1 - t0
+            t_dec += t2 - t1
+            passes += 1
     finally:
         L.or_set_simd(0)
-    gib = Gs * k * S / 2**30
-    return {"value": round(gib / (t2 - t0), 3), "unit": "GiB/s", "cores": threads,
+    gib = passes * Gs * k * S / 2**30
+    return {"value": round(gib / (t_enc + t_dec), 3), "unit": "GiB/s", "cores": threads,
             "kind": "port",
-            "sample": f"{Gs} generations k={k} r={r} S={S} m={m}, encode+decode, AVX2 "
-                      f"split-nibble oracle path, {threads} threads, {t2 - t0:.1f}s",
-            "encode_s": round(t1 - t0, 3), "decode_s": round(t2 - t1, 3)}
+            "sample": f"{passes} x {Gs} generations k={k} r={r} S={S} m={m}, encode+decode, AVX2 "
+                      f"split-nibble oracle path (gf-complete w=8 algorithm class), {threads} "
+                      f"threads, {t_enc + t_dec:.1f}s wall",
+            "encode_s": round(t_enc, 3), "decode_s": round(t_dec, 3)}
 
 
 def main():
@@ -233,9 +242,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from netcode_amd.shard import max_over_ranks
+        elapsed = max_over_ranks(elapsed, dist, dev)
 
     t_enc, t_plan, t_apply = w.kernel_times()
     ms_step = elapsed / a.steps * 1e3

@@ -30,8 +30,8 @@
 
 namespace ntcgpu {
 
-__constant__ PermTables d_perm = make_perm_tables();
-__constant__ FieldTables d_field = make_field_tables();
+__constant__ __attribute__((aligned(16))) PermTables d_perm = make_perm_tables();
+__constant__ __attribute__((aligned(16))) FieldTables d_field = make_field_tables();
 
 constexpr int kWaves = 4;               // waves per 256-thread block
 constexpr int kMaxPlanRows = 64;        // m <= 64 (r <= 64) in this build
@@ -442,14 +442,12 @@ __device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
          __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
 }
 
-constexpr int kPitchW = (2 * kMaxPlanRows) / 4 + 1;   // dwords per augmented row (odd: no bank conflicts)
 
 // D rows for four received-source positions (one lane): acc[s] holds D[s][p0..p0+3] as bytes.
-template <int R>
+template <int R, int RM>
 __device__ __forceinline__ void plan_dmac(uint32_t m, uint32_t p0, uint32_t nb, uint32_t sidb,
                                           const uint16_t* rl, const uint32_t* rq1,
-                                          const uint16_t (*mA)[kMaxPlanRows],
-                                          const uint32_t (*ptab)[8], uint8_t* dst, uint32_t rp)
+                                          const uint16_t (*mA)[RM], uint8_t* dst, uint32_t rp)
 {
   uint32_t S1[4];
 #pragma unroll
@@ -466,7 +464,7 @@ __device__ __forceinline__ void plan_dmac(uint32_t m, uint32_t p0, uint32_t nb, 
     const uint16_t* row = mA[q];
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-      const uint32_t* tb = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(ptab) + row[t]);
+      const uint32_t* tb = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&d_perm.w[0][0]) + row[t]);
       const uint4 ab = *reinterpret_cast<const uint4*>(tb);
       const uint32_t e = tb[4];
       acc[t] ^= xor3(__builtin_amdgcn_perm(ab.y, ab.x, sa), __builtin_amdgcn_perm(ab.w, ab.z, sb),
@@ -486,27 +484,35 @@ __device__ __forceinline__ void plan_dmac(uint32_t m, uint32_t p0, uint32_t nb, 
   (void)m;
 }
 
+// RM = row bound of this instantiation (r <= RM): sizes LDS and registers to the launch, so
+// small generations keep many waves per CU (the plan is latency-bound).
+template <int RM>
 __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
 {
-  __shared__ uint8_t exp_t[512];
-  __shared__ uint8_t log_t[256];
-  __shared__ uint32_t A[kMaxPlanRows][kPitchW];       // augmented [M | I], row q = repair q
-  __shared__ uint16_t miss[kMaxPlanRows];
-  __shared__ uint16_t recv[kMaxPlanRows];
-  __shared__ uint16_t reps[kMaxPlanRows];
-  __shared__ uint16_t mA[kMaxPlanRows][kMaxPlanRows];   // 32 * (M^-1)[s][q], [q][s]
-  __shared__ uint32_t rq1[kMaxPlanRows];
-  __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
-  __shared__ uint16_t rl[1024];
-  __shared__ uint16_t sl[1024];
-  __shared__ uint16_t rszL[kMaxPlanRows];
-  __shared__ uint32_t szs[kMaxPlanRows];
+  constexpr int kPitchW = (2 * RM) / 4 + 1;   // dwords per augmented row (odd: no bank conflicts)
+  constexpr int kChunk = 256;                 // received sources staged per pass
+  __shared__ __attribute__((aligned(16))) uint8_t exp_t[512];
+  __shared__ __attribute__((aligned(16))) uint8_t log_t[256];
+  __shared__ uint32_t A[RM][kPitchW];          // augmented [M | I], row q = repair q
+  __shared__ uint16_t miss[RM];
+  __shared__ uint16_t recv[RM];
+  __shared__ uint16_t reps[RM];
+  __shared__ uint16_t mA[RM][RM];              // 32 * (M^-1)[s][q], [q][s]
+  __shared__ uint32_t rq1[RM];
+  __shared__ uint16_t rl[kChunk];
+  __shared__ uint16_t sl[kChunk];
+  __shared__ uint16_t rszL[RM];
+  __shared__ uint32_t szs[RM];
 
   const uint32_t lane = threadIdx.x;
   const uint32_t g = blockIdx.x;
-  for (uint32_t t = lane; t < 512; t += 64) exp_t[t] = d_field.exp[t];
-  for (uint32_t t = lane; t < 256; t += 64) log_t[t] = d_field.log[t];
-  for (uint32_t t = lane; t < 256 * 8; t += 64) ptab[t / 8][t % 8] = d_perm.w[t / 8][t % 8];
+  {
+    const uint4* fe = reinterpret_cast<const uint4*>(d_field.exp);
+    const uint4* fl = reinterpret_cast<const uint4*>(d_field.log);
+    const uint4 ve = lane < 32 ? fe[lane] : fl[(lane - 32) & 15];
+    if (lane < 32) reinterpret_cast<uint4*>(exp_t)[lane] = ve;
+    else if (lane < 48) reinterpret_cast<uint4*>(log_t)[lane - 32] = ve;
+  }
   // galois_field::multiply_size (galois_field.hh:108-115) on the LDS tables
   auto msize = [&](uint32_t size, uint32_t c) -> uint32_t {
     if (size == 0 || c == 0) return 0u;
@@ -521,6 +527,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
   const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  if (a.ablate & 8u) return;
 
   uint32_t m = 0;
   for (uint32_t base = 0; base < k; base += 64) {
@@ -529,7 +536,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
     const uint64_t b = __ballot(lost);
     if (lost) {
       const uint32_t pos = m + __popcll(b & lt);
-      if (pos < kMaxPlanRows) miss[pos] = static_cast<uint16_t>(idx);
+      if (pos < RM) miss[pos] = static_cast<uint16_t>(idx);
     }
     m += __popcll(b);
   }
@@ -541,12 +548,13 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
     const uint64_t b = __ballot(got);
     if (got) {
       const uint32_t pos = nrecv + __popcll(b & lt);
-      if (pos < kMaxPlanRows) recv[pos] = static_cast<uint16_t>(idx);
+      if (pos < RM) recv[pos] = static_cast<uint16_t>(idx);
     }
     nrecv += __popcll(b);
   }
   __syncthreads();
 
+  if (a.ablate & 4u) return;
   ntc_gf256_decode_status st{};
   st.nb_missing = static_cast<uint16_t>(m);
   st.last_repair = 0xFFFF;
@@ -555,7 +563,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   if (m == 0) {
     st.state = 1;
     st.nb_useless = static_cast<uint16_t>(nrecv);
-  } else if (nrecv < m || m > kMaxPlanRows) {
+  } else if (nrecv < m || m > static_cast<uint32_t>(RM)) {
     st.state = 2;
   } else {
     const uint32_t nw = (2 * m + 3) / 4;   // dwords per augmented row in use
@@ -597,7 +605,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         }
         // normalise row p by 1/pivot (uniform coefficient table)
         const uint32_t piv = (A[p][pw] >> ps) & 0xFFu;
-        const uint32_t* ti = ptab[exp_t[(255 - log_t[piv]) % 255]];
+        const uint32_t* ti = d_perm.w[exp_t[(255 - log_t[piv]) % 255]];
         for (uint32_t w = lane; w < nw; w += 64) A[p][w] = mul4(ti, A[p][w]);
         __syncthreads();
         // eliminate column p from every other row: lane = row, per-lane table of its factor
@@ -605,7 +613,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         if (fa != 0) {
           uint32_t tf[5];
 #pragma unroll
-          for (int e = 0; e < 5; ++e) tf[e] = ptab[fa][e];
+          for (int e = 0; e < 5; ++e) tf[e] = d_perm.w[fa][e];
           for (uint32_t w = 0; w < nw; ++w) A[lane][w] ^= mul4(tf, A[p][w]);
         }
         __syncthreads();
@@ -644,7 +652,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         rq1[lane] = ridb + reps[lane] + 1u;
         szs[lane] = rszL[reps[lane]];           // becomes the reduced encoded size of repair q
       }
-      const uint32_t R = m <= 8 ? 8u : m <= 16 ? 16u : m <= 32 ? 32u : 64u;
+      const uint32_t R = m <= 8 ? 8u : m <= 16 ? 16u : m <= 32 ? 32u : 64u;   // <= RM
       for (uint32_t idx = lane; idx < m * R; idx += 64) {
         const uint32_t q = idx / R, srow = idx % R;
         mA[q][srow] = static_cast<uint16_t>(srow < m ? 32u * minv(srow, q) : 0u);
@@ -653,8 +661,8 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
       // Positions m..k-1: received sources ascending; D[s][j] = sum_q (M^-1)[s][q] * c(rep_q, j),
       // computed as a small v_perm MAC (lane = 4 consecutive positions, x = their coefficients).
       uint32_t pos_base = m;
-      for (uint32_t cbase = 0; cbase < k; cbase += 1024) {
-        const uint32_t cend = min(k, cbase + 1024);
+      for (uint32_t cbase = 0; cbase < k; cbase += kChunk) {
+        const uint32_t cend = min(k, cbase + static_cast<uint32_t>(kChunk));
         uint32_t cnt = 0;
         for (uint32_t b2 = cbase; b2 < cend; b2 += 64) {
           const uint32_t j = b2 + lane;
@@ -683,10 +691,14 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
           for (uint32_t p0 = 4 * lane; p0 < cnt; p0 += 256) {
             uint8_t* dst = pc + static_cast<size_t>(pos_base + p0) * a.rp;
             const uint32_t nb = min(4u, cnt - p0);
-            if (R == 8) plan_dmac<8>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
-            else if (R == 16) plan_dmac<16>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
-            else if (R == 32) plan_dmac<32>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
-            else plan_dmac<64>(m, p0, nb, sidb, rl, rq1, mA, ptab, dst, a.rp);
+            if (R == 8 || RM == 8) plan_dmac<8, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+            else if constexpr (RM >= 16) {
+              if (R == 16 || RM == 16) plan_dmac<16, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+              else if constexpr (RM >= 32) {
+                if (R == 32 || RM == 32) plan_dmac<32, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+                else if constexpr (RM >= 64) plan_dmac<64, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+              }
+            }
           }
         }
         pos_base += cnt;
@@ -777,13 +789,9 @@ int pick_d(uint32_t stride)
     return v ? std::atoi(v) : 0;
   }();
   if ((forced == 1 || forced == 2 || forced == 4) && stride % (4u * forced) == 0) return forced;
-  // Prefer 16 B per lane (dwordx4) unless the last column chunk would leave >10 % of lanes idle.
-  for (int D = 4; D >= 2; D /= 2) {
-    const uint32_t span = 256u * D;
-    const uint32_t chunks = (stride + span - 1) / span;
-    if (stride % (4u * D) == 0 && 10ull * stride >= 9ull * chunks * span) return D;
-  }
-  return stride % 8 == 0 && stride >= 512 ? 2 : 1;
+  // 8 B per lane measured fastest on MI355X for 1-4 KiB symbols (more waves per SIMD at the same
+  // per-coefficient table cost); 4 B only when the stride forces it.
+  return stride % 8 == 0 ? 2 : 1;
 }
 
 typedef void (*mac_fn)(MacArgs);
@@ -968,7 +976,8 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
   p.ablate = ablate;
-  hipLaunchKernelGGL(decode_plan, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
+  auto* fn = r <= 8 ? decode_plan<8> : r <= 16 ? decode_plan<16> : r <= 32 ? decode_plan<32> : decode_plan<64>;
+  hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
   return hip_check(hipGetLastError(), "decode_plan launch");
 }

@@ -1,0 +1,22 @@
+/* netcode/c/data.h -- application data buffers (reference netcode/c/data.h:30-85). */
+#ifndef NETCODE_C_DATA_H
+#define NETCODE_C_DATA_H
+#include "netcode/c/error.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ntc_data_t ntc_data_t;
+
+ntc_data_t* ntc_new_data(uint16_t size) NTC_C_NOEXCEPT;                  /* NULL on OOM */
+ntc_data_t* ntc_new_data_from(const char* src, uint16_t size) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void        ntc_delete_data(ntc_data_t* data) NTC_C_NOEXCEPT NTC_C_NONNULL;
+char*       ntc_data_buffer(ntc_data_t* data) NTC_C_NOEXCEPT NTC_C_NONNULL;   /* 16-B aligned */
+uint16_t    ntc_data_get_size(const ntc_data_t* data) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void        ntc_data_resize(ntc_data_t* data, uint16_t new_size, ntc_error* error)
+            NTC_C_NOEXCEPT NTC_C_NONNULL;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,28 @@
+/* netcode/c/ext.h -- introspection extensions of the MI355X build (not in the reference C ABI).
+ * Exposes the counters the reference keeps on ntc::encoder / ntc::decoder (encoder.hh:114-143,
+ * decoder.hh:157-210) so C callers and tests can read them. */
+#ifndef NETCODE_C_EXT_H
+#define NETCODE_C_EXT_H
+#include "netcode/c/decoder.h"
+#include "netcode/c/encoder.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  NTC_ENC_NB_SENT_REPAIRS = 0, NTC_ENC_NB_SENT_SOURCES = 1, NTC_ENC_NB_RECEIVED_ACKS = 2,
+  NTC_ENC_RATE = 3, NTC_ENC_WINDOW = 4
+};
+enum {
+  NTC_DEC_NB_DECODED = 0, NTC_DEC_NB_FAILED_FULL_DECODINGS = 1, NTC_DEC_NB_MISSING_SOURCES = 2,
+  NTC_DEC_NB_RECEIVED_REPAIRS = 3, NTC_DEC_NB_RECEIVED_SOURCES = 4, NTC_DEC_NB_SENT_ACKS = 5,
+  NTC_DEC_NB_USELESS_REPAIRS = 6, NTC_DEC_NB_PENDING_REPAIRS = 7
+};
+
+size_t ntc_encoder_counter(const ntc_encoder_t* enc, int which) NTC_C_NOEXCEPT NTC_C_NONNULL;
+size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT NTC_C_NONNULL;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

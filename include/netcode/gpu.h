@@ -98,6 +98,16 @@ int  ntc_gf256_decode_plan(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32
 int  ntc_gf256_decode_apply(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
                             uint32_t stride, uint8_t* src, const uint8_t* rep, void* stream);
 
+/* General batched combination with caller-supplied coefficients (no id schedule):
+ *   out[g][j] = sum_i coef[g][i][j] * in[g][i]      (j < rows, i < k), over `stride` bytes,
+ * coef laid out [G][k][ntc_gf256_coef_pitch(rows)] bytes (entries j >= rows ignored).  Used by
+ * the per-packet netcode/c layer (one repair or one decoded source = one row) and by dense
+ * non-reference codes (BASELINE config 5). */
+uint32_t ntc_gf256_coef_pitch(uint32_t rows);
+int  ntc_gf256_combine_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t rows,
+                             uint32_t stride, const uint8_t* in, const uint8_t* coef,
+                             uint8_t* out, void* stream);
+
 /* dst = c*src (add = 0) or dst ^= c*src (add = 1) over `len` bytes of device memory. */
 int  ntc_gf256_region_multiply(ntc_gf256_engine* eng, const uint8_t* src, uint8_t* dst,
                                size_t len, uint8_t c, int add, void* stream);

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "libntc_gf256.so")
 GPU_H_SYMBOLS = [
     "ntc_gf256_engine_create", "ntc_gf256_engine_destroy", "ntc_gf256_reserve",
     "ntc_gf256_encode_batch", "ntc_gf256_decode_batch", "ntc_gf256_decode_plan",
-    "ntc_gf256_decode_apply", "ntc_gf256_region_multiply", "ntc_gf256_coefficient",
+    "ntc_gf256_decode_apply", "ntc_gf256_region_multiply", "ntc_gf256_coef_pitch",
+    "ntc_gf256_combine_batch", "ntc_gf256_coefficient",
     "ntc_gf256_multiply_size", "ntc_gf256_multiply", "ntc_gf256_invert",
     "ntc_gf256_last_error", "ntc_gf256_build_info",
 ]
@@ -59,6 +60,9 @@ def load(path: str | None = None):
     L.ntc_gf256_decode_plan.argtypes = [V, u32, u32, u32, P, P, P, P, P, P, P, V]
     L.ntc_gf256_decode_apply.argtypes = [V, u32, u32, u32, u32, P, P, V]
     L.ntc_gf256_region_multiply.argtypes = [V, P, P, C.c_size_t, u8, C.c_int, V]
+    L.ntc_gf256_coef_pitch.argtypes = [u32]
+    L.ntc_gf256_coef_pitch.restype = u32
+    L.ntc_gf256_combine_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, V]
     L.ntc_gf256_coefficient.argtypes = [u32, u32]
     L.ntc_gf256_coefficient.restype = u32
     L.ntc_gf256_multiply_size.argtypes = [u16, u32]

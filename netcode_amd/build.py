@@ -14,7 +14,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 TARGETS = {
-    "libntc_gf256.so": ["csrc/ntc_gf256.hip"],
+    # GF(2^8) engine: kernels + batched C ABI (include/netcode/gpu.h)
+    "libntc_gf256.so": (["csrc/ntc_gf256.hip"], []),
+    # reference per-packet C ABI (include/netcode/c/*.h) over the engine
+    "libntc.so": (["csrc/ntc_capi.cpp"], ["-L", "{here}", "-lntc_gf256", "-Wl,-rpath,$ORIGIN"]),
 }
 
 
@@ -24,19 +27,22 @@ def _stale(out: str, srcs: list[str]) -> bool:
     t = os.path.getmtime(out)
     deps = srcs + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))]
     deps.append(os.path.join(ROOT, "include", "netcode", "gpu.h"))
+    cdir = os.path.join(ROOT, "include", "netcode", "c")
+    deps += [os.path.join(cdir, f) for f in os.listdir(cdir)]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
 def build(force: bool = False, verbose: bool = True) -> list[str]:
     built = []
-    for out, srcs in TARGETS.items():
+    for out, (srcs, link) in TARGETS.items():
         out_p = os.path.join(HERE, out)
         srcs_p = [os.path.join(HERE, s) for s in srcs]
+        link = [x.replace("{here}", HERE) for x in link]
         if not force and not _stale(out_p, srcs_p):
             built.append(out_p)
             continue
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out_p + ".tmp"] + srcs_p
+               "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out_p + ".tmp"] + srcs_p + link
         if verbose:
             print("[netcode_amd.build]", " ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

@@ -1,0 +1,910 @@
+// ntc_capi.cpp -- the reference's per-packet C ABI (netcode/c/*.h) on top of the MI355X engine.
+//
+// The protocol state machines (ntc::encoder, ntc::decoder, detail::decoder, packetizer) run on
+// the host exactly as in the reference; every GF(2^8) region operation they issue -- a repair
+// (detail/encoder.cc:15-64), the reduction of a repair by known sources (detail/decoder.cc:
+// 393-408), peeling (:156-178) and full decoding (:480-559) -- is one ntc_gf256_combine_batch
+// launch on the GPU.  There is no CPU fallback: without a HIP device ntc_new_encoder /
+// ntc_new_decoder return NULL and ntc_* calls report an error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <list>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "netcode/c/decoder.h"
+#include "netcode/c/encoder.h"
+#include "netcode/c/ext.h"
+#include "netcode/gpu.h"
+
+namespace ntcx {
+
+// ------------------------------------------------------------------------------ errors ----
+struct packet_type_error : std::runtime_error {
+  packet_type_error() : std::runtime_error("packet type error") {}
+};
+struct overflow_error : std::runtime_error {
+  overflow_error() : std::runtime_error("overflow error") {}
+};
+struct device_error : std::runtime_error {
+  explicit device_error(const std::string& m) : std::runtime_error(m) {}
+};
+
+// --------------------------------------------------------------------- aligned storage ----
+template <typename T>
+struct Align16 {
+  using value_type = T;
+  Align16() = default;
+  template <typename U> Align16(const Align16<U>&) {}
+  T* allocate(size_t n)
+  {
+    void* p = ::operator new(n * sizeof(T) + 0, std::align_val_t(16));
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) { ::operator delete(p, std::align_val_t(16)); }
+  template <typename U> bool operator==(const Align16<U>&) const { return true; }
+  template <typename U> bool operator!=(const Align16<U>&) const { return false; }
+};
+using bytes = std::vector<uint8_t, Align16<uint8_t>>;
+
+// ---------------------------------------------------------------------- device engine ----
+// One engine + stream + staging per process (objects are not thread-safe, like the reference).
+class Device {
+ public:
+  static Device& get()
+  {
+    static Device d;
+    if (!d.eng_) throw device_error(d.err_);
+    return d;
+  }
+
+  // out[0..out_len) = sum_i c_i * in_i[0..len_i)  (inputs zero padded), one launch.
+  void combine(size_t n, const uint8_t* const* in, const uint16_t* lens, const uint8_t* coefs,
+               size_t out_len, uint8_t* out)
+  {
+    size_t mx = out_len;
+    for (size_t i = 0; i < n; ++i) mx = std::max<size_t>(mx, lens[i]);
+    const size_t stride = std::max<size_t>(16, (mx + 15) / 16 * 16);
+    const uint32_t pitch = ntc_gf256_coef_pitch(1);
+    const size_t nin = n ? n : 1;
+    grow(nin * stride, nin * pitch, stride);
+    std::memset(h_in_, 0, nin * stride);
+    std::memset(h_coef_, 0, nin * pitch);
+    for (size_t i = 0; i < n; ++i) {
+      std::memcpy(h_in_ + i * stride, in[i], lens[i]);
+      h_coef_[i * pitch] = coefs[i];
+    }
+    check(hipMemcpyAsync(d_in_, h_in_, nin * stride, hipMemcpyHostToDevice, stream_), "H2D");
+    check(hipMemcpyAsync(d_coef_, h_coef_, nin * pitch, hipMemcpyHostToDevice, stream_), "H2D");
+    const int rc = ntc_gf256_combine_batch(eng_, 1, static_cast<uint32_t>(nin), 1,
+                                           static_cast<uint32_t>(stride), d_in_, d_coef_, d_out_,
+                                           stream_);
+    if (rc) throw device_error(ntc_gf256_last_error());
+    check(hipMemcpyAsync(h_out_, d_out_, stride, hipMemcpyDeviceToHost, stream_), "D2H");
+    check(hipStreamSynchronize(stream_), "sync");
+    std::memcpy(out, h_out_, out_len);
+  }
+
+  // Several outputs from the same inputs: out_s = sum_i coef[i][s] * in_i (full decoding).
+  void combine_rows(size_t n, const uint8_t* const* in, const uint16_t* lens, size_t rows,
+                    const uint8_t* coef /*[n][rows]*/, size_t out_len, uint8_t* const* out)
+  {
+    size_t mx = out_len;
+    for (size_t i = 0; i < n; ++i) mx = std::max<size_t>(mx, lens[i]);
+    const size_t stride = std::max<size_t>(16, (mx + 15) / 16 * 16);
+    const uint32_t pitch = ntc_gf256_coef_pitch(static_cast<uint32_t>(rows));
+    grow(n * stride, n * pitch, rows * stride);
+    std::memset(h_in_, 0, n * stride);
+    std::memset(h_coef_, 0, n * pitch);
+    for (size_t i = 0; i < n; ++i) {
+      std::memcpy(h_in_ + i * stride, in[i], lens[i]);
+      for (size_t s = 0; s < rows; ++s) h_coef_[i * pitch + s] = coef[i * rows + s];
+    }
+    check(hipMemcpyAsync(d_in_, h_in_, n * stride, hipMemcpyHostToDevice, stream_), "H2D");
+    check(hipMemcpyAsync(d_coef_, h_coef_, n * pitch, hipMemcpyHostToDevice, stream_), "H2D");
+    const int rc = ntc_gf256_combine_batch(eng_, 1, static_cast<uint32_t>(n),
+                                           static_cast<uint32_t>(rows),
+                                           static_cast<uint32_t>(stride), d_in_, d_coef_, d_out_,
+                                           stream_);
+    if (rc) throw device_error(ntc_gf256_last_error());
+    check(hipMemcpyAsync(h_out_, d_out_, rows * stride, hipMemcpyDeviceToHost, stream_), "D2H");
+    check(hipStreamSynchronize(stream_), "sync");
+    for (size_t s = 0; s < rows; ++s) std::memcpy(out[s], h_out_ + s * stride, out_len);
+  }
+
+  uint64_t launches() const { return launches_; }
+
+ private:
+  Device()
+  {
+    const char* v = std::getenv("NTC_DEVICE");
+    const int dev = v ? std::atoi(v) : 0;
+    if (ntc_gf256_engine_create(dev, &eng_) != 0) {
+      err_ = std::string("no MI355X engine: ") + ntc_gf256_last_error();
+      eng_ = nullptr;
+      return;
+    }
+    if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+      err_ = "hipStreamCreate failed";
+      ntc_gf256_engine_destroy(eng_);
+      eng_ = nullptr;
+    }
+  }
+  ~Device()
+  {
+    // Process teardown: the HIP runtime may already be gone; release best effort.
+  }
+  static void check(hipError_t e, const char* what)
+  {
+    if (e != hipSuccess) throw device_error(std::string(what) + ": " + hipGetErrorString(e));
+  }
+  void grow(size_t in_bytes, size_t coef_bytes, size_t out_bytes)
+  {
+    auto up = [](void** d, void** h, size_t* cap, size_t need) {
+      if (need <= *cap) return;
+      const size_t n = std::max(need, *cap * 2);
+      if (*d) (void)hipFree(*d);
+      if (*h) (void)hipHostFree(*h);
+      *d = nullptr;
+      *h = nullptr;
+      *cap = 0;
+      check(hipMalloc(d, n), "hipMalloc");
+      check(hipHostMalloc(h, n, hipHostMallocDefault), "hipHostMalloc");
+      *cap = n;
+    };
+    up(reinterpret_cast<void**>(&d_in_), reinterpret_cast<void**>(&h_in_), &cap_in_, in_bytes);
+    up(reinterpret_cast<void**>(&d_coef_), reinterpret_cast<void**>(&h_coef_), &cap_coef_, coef_bytes + 64);
+    up(reinterpret_cast<void**>(&d_out_), reinterpret_cast<void**>(&h_out_), &cap_out_, out_bytes);
+    ++launches_;
+  }
+
+  ntc_gf256_engine* eng_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  std::string err_;
+  uint8_t *d_in_ = nullptr, *h_in_ = nullptr, *d_coef_ = nullptr, *h_coef_ = nullptr;
+  uint8_t *d_out_ = nullptr, *h_out_ = nullptr;
+  size_t cap_in_ = 0, cap_coef_ = 0, cap_out_ = 0;
+  uint64_t launches_ = 0;
+};
+
+inline uint8_t coef(uint32_t rid, uint32_t sid) { return static_cast<uint8_t>(ntc_gf256_coefficient(rid, sid)); }
+inline uint16_t msize(uint16_t s, uint32_t c) { return ntc_gf256_multiply_size(s, c); }
+inline uint32_t gmul(uint32_t a, uint32_t b) { return ntc_gf256_multiply(static_cast<uint8_t>(a), static_cast<uint8_t>(b)); }
+
+// --------------------------------------------------------------------------- wire format ----
+// Big-endian fields; id lists RLE-coded on 16-bit deltas (detail/packetizer.hh:263-352).
+struct Writer {
+  ntc_packet_handler h;
+  void raw(const void* p, size_t n) { h.prepare_packet(h.context, static_cast<const char*>(p), n); }
+  void u8(uint8_t x) { raw(&x, 1); }
+  void u16(uint16_t x) { const uint8_t b[2] = {uint8_t(x >> 8), uint8_t(x)}; raw(b, 2); }
+  void u32(uint32_t x)
+  {
+    const uint8_t b[4] = {uint8_t(x >> 24), uint8_t(x >> 16), uint8_t(x >> 8), uint8_t(x)};
+    raw(b, 4);
+  }
+  void ids(const std::vector<uint32_t>& v)      // packetizer.hh:263-309
+  {
+    if (v.empty()) { u16(0); return; }
+    std::vector<std::pair<uint8_t, uint16_t>> rle;
+    size_t c = 1;
+    while (c < v.size()) {
+      uint8_t run = 1;
+      const uint32_t d = v[c] - v[c - 1];
+      while (c + 1 < v.size() && v[c + 1] - v[c] == d && run < 255) { ++run; ++c; }
+      rle.emplace_back(run, static_cast<uint16_t>(d));
+      ++c;
+    }
+    u16(static_cast<uint16_t>(rle.size() + 1));
+    u32(v[0]);
+    for (const auto& p : rle) { u8(p.first); u16(p.second); }
+  }
+  void end() { h.send_packet(h.context); }
+};
+
+struct Reader {
+  const uint8_t* p;
+  size_t left;
+  uint8_t u8() { need(1); const uint8_t x = p[0]; p += 1; left -= 1; return x; }
+  uint16_t u16() { need(2); const uint16_t x = uint16_t((p[0] << 8) | p[1]); p += 2; left -= 2; return x; }
+  uint32_t u32()
+  {
+    need(4);
+    const uint32_t x = (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | p[3];
+    p += 4; left -= 4;
+    return x;
+  }
+  const uint8_t* skip(size_t n) { need(n); const uint8_t* q = p; p += n; left -= n; return q; }
+  void need(size_t n) const { if (left < n) throw overflow_error(); }
+  std::vector<uint32_t> ids()                   // packetizer.hh:312-352 (sorted, unique)
+  {
+    std::set<uint32_t> s;
+    const uint16_t ne = u16();
+    if (ne == 0) return {};
+    uint32_t acc = u32();
+    s.insert(acc);
+    for (uint32_t i = 0; i + 1u < ne; ++i) {
+      const uint8_t run = u8();
+      const uint16_t d = u16();
+      for (uint32_t j = 0; j < run; ++j) { acc += d; s.insert(acc); }
+    }
+    return std::vector<uint32_t>(s.begin(), s.end());
+  }
+};
+
+}  // namespace ntcx
+
+// ====================================================================== C ABI objects ======
+struct ntc_data_t {
+  ntcx::bytes v;
+};
+
+struct ntc_packet_t {
+  static constexpr size_t shift = 9;   // 16 - 7-byte header (packet.hh:30-36)
+  ntcx::bytes v;
+  explicit ntc_packet_t(size_t n) : v(n + shift, 0) {}
+  uint8_t* data() { return v.data() + shift; }
+  size_t size() const { return v.size() - shift; }
+};
+
+namespace ntcx {
+
+// ============================================================================== encoder ====
+class Encoder {
+ public:
+  Encoder(uint8_t w, ntc_packet_handler h) : out_{h}
+  {
+    if (w != 8) throw std::invalid_argument("this build implements GF(2^8) only");
+    Device::get();
+  }
+
+  // encoder.hh:255-285
+  void add_data(bytes&& d)
+  {
+    if (window_.size() == window_size_) window_.pop_front();
+    window_.push_back(Src{cur_sid_, std::move(d)});
+    const Src& s = window_.back();
+    if (systematic_) {
+      ++nb_sources_;
+      ++nb_sent_packets_;
+      out_.u8(2);                                  // packetizer.hh:165-183
+      out_.u32(s.id);
+      out_.u16(static_cast<uint16_t>(s.sym.size()));
+      out_.raw(s.sym.data(), s.sym.size());
+      out_.end();
+    } else {
+      generate_repair();
+    }
+    if ((cur_sid_ + 1) % rate_ == 0) generate_repair();
+    ++cur_sid_;
+  }
+
+  // encoder.hh:162-169, 321-333 + detail/encoder.cc:15-64 (the combination runs on the GPU)
+  void generate_repair()
+  {
+    if (window_.empty()) throw std::runtime_error("generate_repair on an empty window");
+    std::vector<const uint8_t*> in;
+    std::vector<uint16_t> lens;
+    std::vector<uint8_t> cs;
+    std::vector<uint32_t> ids;
+    uint16_t symsz = 0, esz = 0;
+    for (const Src& s : window_) {
+      const uint8_t c = coef(cur_rid_, s.id);
+      in.push_back(s.sym.data());
+      lens.push_back(static_cast<uint16_t>(s.sym.size()));
+      cs.push_back(c);
+      ids.push_back(s.id);
+      symsz = std::max<uint16_t>(symsz, static_cast<uint16_t>(s.sym.size()));
+      esz = static_cast<uint16_t>(msize(static_cast<uint16_t>(s.sym.size()), c) ^ esz);
+    }
+    bytes sym(symsz);
+    Device::get().combine(in.size(), in.data(), lens.data(), cs.data(), symsz, sym.data());
+    const uint32_t rid = cur_rid_++;
+    ++nb_repairs_;
+    ++nb_sent_packets_;
+    out_.u8(1);                                    // packetizer.hh:90-122
+    out_.u32(rid);
+    out_.u16(symsz);
+    out_.raw(sym.data(), symsz);
+    out_.ids(ids);
+    out_.u16(esz);
+    out_.u16(symsz);
+    out_.raw(sym.data(), symsz);
+    out_.end();
+  }
+
+  // encoder.hh:290-318 + packetizer.hh:64-88 + source_list.hh:34-60
+  size_t add_packet(const uint8_t* p, size_t n)
+  {
+    if (n == 0) throw overflow_error();
+    if (p[0] != 0) throw packet_type_error();
+    ++nb_acks_;
+    Reader r{p, n};
+    r.u8();
+    const uint16_t nbp = r.u16();
+    const std::vector<uint32_t> ids = r.ids();
+    if (adaptive_) {
+      double loss = 0.0;
+      if (nb_sent_packets_ > 0)
+        loss = static_cast<double>(int(nb_sent_packets_) - int(nbp)) / static_cast<double>(nb_sent_packets_);
+      rate_ = loss < 0.01 ? 50 : static_cast<size_t>(std::ceil((1.0 / loss) / 2.0));
+    }
+    nb_sent_packets_ = 0;
+    auto it = window_.begin();
+    size_t ii = 0;
+    while (it != window_.end() && ii < ids.size()) {
+      if (it->id == ids[ii]) { it = window_.erase(it); ++ii; }
+      else if (it->id > ids[ii]) ++ii;
+      else ++it;
+    }
+    return n - r.left;
+  }
+
+  size_t window() const { return window_.size(); }
+  void set_rate(size_t r) { if (r) rate_ = r; }
+  void set_window_size(size_t s) { if (s) window_size_ = s; }
+  void set_systematic(bool s) { systematic_ = s; }
+  void set_adaptive(bool a) { adaptive_ = a; }
+  size_t counter(int which) const
+  {
+    switch (which) {
+      case NTC_ENC_NB_SENT_REPAIRS: return nb_repairs_;
+      case NTC_ENC_NB_SENT_SOURCES: return nb_sources_;
+      case NTC_ENC_NB_RECEIVED_ACKS: return nb_acks_;
+      case NTC_ENC_RATE: return rate_;
+      case NTC_ENC_WINDOW: return window_.size();
+      default: return 0;
+    }
+  }
+
+ private:
+  struct Src {
+    uint32_t id;
+    bytes sym;
+  };
+  Writer out_;
+  std::list<Src> window_;
+  size_t rate_ = 5;
+  size_t window_size_ = static_cast<size_t>(-1);
+  bool systematic_ = true;
+  bool adaptive_ = false;
+  uint32_t cur_sid_ = 0, cur_rid_ = 0;
+  size_t nb_repairs_ = 0, nb_acks_ = 0, nb_sources_ = 0;
+  uint16_t nb_sent_packets_ = 0;
+};
+
+// ============================================================================== decoder ====
+// detail/decoder.{hh,cc} semantics; host containers, GPU region work.
+class Decoder {
+ public:
+  Decoder(uint8_t w, bool in_order, ntc_packet_handler ph, ntc_data_handler dh)
+      : in_order_(in_order), out_{ph}, dh_(dh), last_ack_(std::chrono::steady_clock::now())
+  {
+    if (w != 8) throw std::invalid_argument("this build implements GF(2^8) only");
+    Device::get();
+  }
+
+  // decoder.hh:88-122
+  size_t add_packet(const uint8_t* p, size_t n)
+  {
+    if (n == 0) throw overflow_error();
+    Reader rd{p, n};
+    const uint8_t ty = rd.u8();
+    if (ty == 1) {
+      ++nb_rrep_;
+      ++ack_packets_;
+      const uint32_t id = rd.u32();
+      const uint16_t symsz = rd.u16();
+      const uint8_t* sym = rd.skip(symsz);
+      std::vector<uint32_t> ids = rd.ids();
+      const uint16_t esz = rd.u16();
+      const size_t consumed = n - rd.left;
+      if (!ids.empty()) on_repair(id, std::move(ids), esz, sym, symsz);
+      return consumed;
+    }
+    if (ty == 2) {
+      ++nb_rsrc_;
+      ++ack_packets_;
+      const uint32_t id = rd.u32();
+      const uint16_t sz = rd.u16();
+      const uint8_t* sym = rd.skip(sz);
+      const size_t consumed = n - rd.left;
+      on_source(id, sym, sz);
+      return consumed;
+    }
+    throw packet_type_error();
+  }
+
+  // decoder.hh:213-228
+  void generate_ack()
+  {
+    std::vector<uint32_t> ids;
+    ids.reserve(sources_.size());
+    for (const auto& kv : sources_) ids.push_back(kv.first);
+    out_.u8(0);
+    out_.u16(ack_packets_);
+    out_.ids(ids);
+    out_.end();
+    ++nb_acks_;
+    ack_packets_ = 0;
+  }
+
+  void set_ack_period(size_t ms) { ack_period_ms_ = ms; }
+  void set_ack_nb_packets(uint16_t nb) { if (nb) ack_nb_packets_ = std::min<uint16_t>(nb, 128); }
+
+  size_t counter(int which) const
+  {
+    switch (which) {
+      case NTC_DEC_NB_DECODED: return nb_decoded_;
+      case NTC_DEC_NB_FAILED_FULL_DECODINGS: return nb_failed_;
+      case NTC_DEC_NB_MISSING_SOURCES: return missing_.size();
+      case NTC_DEC_NB_RECEIVED_REPAIRS: return nb_rrep_;
+      case NTC_DEC_NB_RECEIVED_SOURCES: return nb_rsrc_;
+      case NTC_DEC_NB_SENT_ACKS: return nb_acks_;
+      case NTC_DEC_NB_USELESS_REPAIRS: return nb_useless_;
+      case NTC_DEC_NB_PENDING_REPAIRS: return repairs_.size();
+      default: return 0;
+    }
+  }
+
+ private:
+  struct Src {
+    uint32_t id;
+    bytes sym;
+    uint16_t size;
+  };
+  struct Rep {
+    uint32_t id;
+    std::vector<uint32_t> ids;   // sorted
+    uint16_t esz;
+    bytes sym;
+    uint16_t symsz;
+  };
+
+  // decoder.hh:231-248, 292-300
+  void deliver(const Src& s)
+  {
+    dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.sym.data()), s.size);
+    if (ack_packets_ >= ack_nb_packets_) {
+      generate_ack();
+      last_ack_ = std::chrono::steady_clock::now();
+    } else if (ack_period_ms_ != 0) {
+      const auto now = std::chrono::steady_clock::now();
+      if (now - last_ack_ >= std::chrono::milliseconds(ack_period_ms_)) {
+        generate_ack();
+        last_ack_ = now;
+      }
+    }
+  }
+  void deliver_id(uint32_t id)
+  {
+    auto it = sources_.find(id);
+    if (it != sources_.end()) deliver(it->second);
+  }
+
+  // detail/decoder.cc:570-591
+  void flush_ordered()
+  {
+    auto it = ordered_.find(first_missing_);
+    if (it == ordered_.end()) return;
+    for (;;) {
+      deliver_id(*it);
+      it = ordered_.erase(it);
+      first_missing_ += 1;
+      if (it == ordered_.end() || *it > first_missing_) break;
+    }
+  }
+
+  // detail/decoder.cc:393-408 for several known sources at once (XOR order is irrelevant).
+  void remove_sources_data(Rep& r, const std::vector<const Src*>& known)
+  {
+    if (known.empty()) return;
+    std::vector<const uint8_t*> in{r.sym.data()};
+    std::vector<uint16_t> lens{r.symsz};
+    std::vector<uint8_t> cs{1};
+    for (const Src* s : known) {
+      const uint8_t c = coef(r.id, s->id);
+      r.esz = static_cast<uint16_t>(msize(s->size, c) ^ r.esz);
+      in.push_back(s->sym.data());
+      lens.push_back(std::min<uint16_t>(s->size, r.symsz));
+      cs.push_back(c);
+    }
+    Device::get().combine(in.size(), in.data(), lens.data(), cs.data(), r.symsz, r.sym.data());
+  }
+
+  // detail/decoder.cc:156-178
+  Src create_source_from_repair(const Rep& r)
+  {
+    const uint32_t sid = r.ids.front();
+    const uint8_t inv = ntc_gf256_invert(coef(r.id, sid));
+    const uint16_t sz = msize(r.esz, inv);
+    Src s{sid, bytes(std::max<size_t>(sz, 1), 0), sz};
+    const uint8_t* in = r.sym.data();
+    const uint16_t len = std::min(sz, r.symsz);
+    Device::get().combine(1, &in, &len, &inv, sz, s.sym.data());
+    nb_decoded_ += 1;
+    return s;
+  }
+
+  // detail/decoder.cc:33-50
+  void on_source(uint32_t id, const uint8_t* sym, uint16_t sz)
+  {
+    if (has_last_ && id < last_id_) return;
+    if (sources_.count(id)) return;
+    Src s{id, bytes(sym, sym + sz), sz};
+    if (s.sym.empty()) s.sym.resize(1);
+    add_source_recursive(std::move(s));
+    attempt_full_decoding();
+  }
+
+  // detail/decoder.cc:54-152
+  void on_repair(uint32_t id, std::vector<uint32_t>&& ids, uint16_t esz, const uint8_t* sym, uint16_t symsz)
+  {
+    if (has_last_ && ids.back() < last_id_) return;
+    if (repairs_.count(id)) return;
+    drop_outdated(ids.front());
+    bool useless = true;
+    for (uint32_t sid : ids) if (!sources_.count(sid)) { useless = false; break; }
+    if (useless) { ++nb_useless_; return; }
+    Rep& r = repairs_.emplace(id, Rep{id, std::move(ids), esz, bytes(sym, sym + symsz), symsz}).first->second;
+    if (r.sym.empty()) r.sym.resize(1);
+    std::vector<const Src*> known;
+    std::vector<uint32_t> remaining;
+    for (auto it = r.ids.rbegin(); it != r.ids.rend(); ++it) {
+      auto s = sources_.find(*it);
+      if (s != sources_.end()) known.push_back(&s->second);
+      else {
+        missing_[*it].insert(id);
+        remaining.push_back(*it);
+      }
+    }
+    remove_sources_data(r, known);
+    std::reverse(remaining.begin(), remaining.end());
+    r.ids = std::move(remaining);
+    if (r.ids.size() == 1) {
+      Src s = create_source_from_repair(r);
+      missing_.erase(s.id);
+      repairs_.erase(id);
+      add_source_recursive(std::move(s));
+      return;
+    }
+    attempt_full_decoding();
+  }
+
+  // detail/decoder.cc:249-337
+  void add_source_recursive(Src&& src)
+  {
+    if (!in_order_) {
+      deliver(src);
+    } else if (src.id == first_missing_) {
+      deliver(src);
+      first_missing_ += 1;
+      flush_ordered();
+    }
+    auto m = missing_.find(src.id);
+    if (m != missing_.end()) {
+      const std::set<uint32_t> rids = m->second;
+      for (uint32_t rid : rids) {
+        auto r = repairs_.find(rid);
+        if (r == repairs_.end()) continue;
+        remove_sources_data(r->second, {&src});
+        auto& v = r->second.ids;
+        v.erase(std::find(v.begin(), v.end(), src.id));
+      }
+      missing_.erase(src.id);
+    }
+    for (auto mit = missing_.begin(); mit != missing_.end();) {
+      if (mit->second.size() == 1) {
+        auto r = repairs_.find(*mit->second.begin());
+        if (r != repairs_.end() && r->second.ids.size() == 1) {
+          Src dec = create_source_from_repair(r->second);
+          const uint32_t cur = mit->first;
+          repairs_.erase(r);
+          missing_.erase(mit);
+          add_source_recursive(std::move(dec));
+          mit = missing_.lower_bound(cur);
+          continue;
+        }
+      }
+      ++mit;
+    }
+    const uint32_t sid = src.id;
+    sources_.emplace(sid, std::move(src));
+    if (in_order_ && sid > first_missing_) ordered_.insert(sid);
+  }
+
+  // detail/decoder.cc:341-389
+  void drop_outdated(uint32_t id)
+  {
+    has_last_ = true;
+    last_id_ = id;
+    for (auto it = repairs_.begin(); it != repairs_.end();) {
+      if (id > it->second.ids.front()) {
+        for (uint32_t sid : it->second.ids) {
+          auto m = missing_.find(sid);
+          if (m != missing_.end()) m->second.erase(it->first);
+        }
+        it = repairs_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    if (in_order_) {
+      while (!ordered_.empty() && *ordered_.begin() < id) {
+        deliver_id(*ordered_.begin());
+        ordered_.erase(ordered_.begin());
+      }
+      if (first_missing_ < id) first_missing_ = id;
+      flush_ordered();
+    }
+    sources_.erase(sources_.begin(), sources_.lower_bound(id));
+    missing_.erase(missing_.begin(), missing_.lower_bound(id));
+  }
+
+  // detail/invert_matrix.cc:9-128 semantics: returns false on a singular matrix (the reference
+  // then reports index rows-1); inv is the unique inverse otherwise.  M is [n][n] row-major,
+  // row = repair, column = missing source (the reference's storage rows).
+  static bool invert(std::vector<uint32_t> M, size_t n, std::vector<uint32_t>& inv)
+  {
+    inv.assign(n * n, 0);
+    for (size_t i = 0; i < n; ++i) inv[i * n + i] = 1;
+    for (size_t i = 0; i < n; ++i) {
+      size_t p = i;
+      while (p < n && M[p * n + i] == 0) ++p;
+      if (p == n) return false;
+      if (p != i)
+        for (size_t k = 0; k < n; ++k) { std::swap(M[i * n + k], M[p * n + k]); std::swap(inv[i * n + k], inv[p * n + k]); }
+      const uint32_t piv = ntc_gf256_invert(static_cast<uint8_t>(M[i * n + i]));
+      for (size_t k = 0; k < n; ++k) { M[i * n + k] = gmul(M[i * n + k], piv); inv[i * n + k] = gmul(inv[i * n + k], piv); }
+      for (size_t j = 0; j < n; ++j) {
+        if (j == i || M[j * n + i] == 0) continue;
+        const uint32_t f = M[j * n + i];
+        for (size_t k = 0; k < n; ++k) { M[j * n + k] ^= gmul(f, M[i * n + k]); inv[j * n + k] ^= gmul(f, inv[i * n + k]); }
+      }
+    }
+    return true;
+  }
+
+  // detail/decoder.cc:412-566
+  void attempt_full_decoding()
+  {
+    if (repairs_.empty() || missing_.empty()) return;
+    if (missing_.size() > repairs_.size()) return;
+    const size_t n = repairs_.size();
+    std::vector<const Rep*> reps;
+    for (const auto& kv : repairs_) reps.push_back(&kv.second);
+    std::vector<uint32_t> mids;
+    for (const auto& kv : missing_) mids.push_back(kv.first);
+    std::vector<uint32_t> M(n * n, 0), inv;
+    for (size_t q = 0; q < n; ++q)
+      for (size_t s = 0; s < n; ++s)
+        if (std::binary_search(reps[q]->ids.begin(), reps[q]->ids.end(), mids[s]))
+          M[q * n + s] = coef(reps[q]->id, mids[s]);
+    if (!invert(M, n, inv)) {                      // :448-468 drop the repair at index rows-1
+      ++nb_failed_;
+      auto last = std::prev(repairs_.end());
+      for (uint32_t sid : last->second.ids) missing_[sid].erase(last->first);
+      repairs_.erase(last);
+      return;
+    }
+    // X = M^-1 R: x_s = sum_q inv[s][q] r_q ; sizes from the reduced encoded sizes (:484-497)
+    std::vector<uint16_t> sizes(n, 0);
+    for (size_t s = 0; s < n; ++s)
+      for (size_t q = 0; q < n; ++q) {
+        const uint32_t c = inv[s * n + q];
+        if (c) sizes[s] = static_cast<uint16_t>(msize(reps[q]->esz, c) ^ sizes[s]);
+      }
+    std::vector<Src> dec(n);
+    std::vector<uint8_t*> outs(n);
+    uint16_t mx = 0;
+    for (size_t s = 0; s < n; ++s) {
+      dec[s] = Src{mids[s], bytes(std::max<size_t>(sizes[s], 1), 0), sizes[s]};
+      outs[s] = dec[s].sym.data();
+      mx = std::max(mx, sizes[s]);
+    }
+    std::vector<const uint8_t*> in(n);
+    std::vector<uint16_t> lens(n);
+    std::vector<uint8_t> cf(n * n);
+    for (size_t q = 0; q < n; ++q) {
+      in[q] = reps[q]->sym.data();
+      lens[q] = reps[q]->symsz;
+      for (size_t s = 0; s < n; ++s) cf[q * n + s] = static_cast<uint8_t>(inv[s * n + q]);
+    }
+    // one launch for all missing sources; bytes past each decoded size are dropped below
+    std::vector<bytes> full(n, bytes(std::max<size_t>(mx, 1), 0));
+    std::vector<uint8_t*> fo(n);
+    for (size_t s = 0; s < n; ++s) fo[s] = full[s].data();
+    Device::get().combine_rows(n, in.data(), lens.data(), n, cf.data(), mx, fo.data());
+    for (size_t s = 0; s < n; ++s) {
+      // the reference reads min(src_sz, repair.symbol_size()) bytes of each repair (:523, :531)
+      std::memcpy(dec[s].sym.data(), full[s].data(), sizes[s]);
+      const uint32_t sid = dec[s].id;
+      sources_.emplace(sid, std::move(dec[s]));
+      if (!in_order_) {
+        deliver_id(sid);
+      } else if (sid == first_missing_) {
+        deliver_id(sid);
+        first_missing_ += 1;
+        flush_ordered();
+      } else {
+        ordered_.insert(sid);
+      }
+    }
+    nb_decoded_ += n;
+    repairs_.clear();
+    missing_.clear();
+  }
+
+  bool in_order_;
+  Writer out_;
+  ntc_data_handler dh_;
+  uint32_t first_missing_ = 0;
+  std::set<uint32_t> ordered_;
+  std::map<uint32_t, Src> sources_;
+  std::map<uint32_t, Rep> repairs_;
+  std::map<uint32_t, std::set<uint32_t>> missing_;
+  bool has_last_ = false;
+  uint32_t last_id_ = 0;
+  size_t nb_useless_ = 0, nb_failed_ = 0, nb_decoded_ = 0;
+  size_t nb_rrep_ = 0, nb_rsrc_ = 0, nb_acks_ = 0;
+  uint16_t ack_packets_ = 0;
+  uint16_t ack_nb_packets_ = 50;
+  size_t ack_period_ms_ = 100;
+  std::chrono::steady_clock::time_point last_ack_;
+};
+
+// c/detail/check_error.hh: exceptions -> ntc_error (message in thread-local storage).
+thread_local std::string t_msg;
+
+template <typename Fn>
+auto guarded(Fn&& fn, ntc_error* error) noexcept -> decltype(fn())
+{
+  error->type = ntc_no_error;
+  try {
+    return fn();
+  } catch (const packet_type_error&) {
+    error->type = ntc_packet_type_error;
+  } catch (const overflow_error&) {
+    error->type = ntc_overflow_error;
+  } catch (const std::bad_alloc&) {
+    error->type = ntc_no_memory;
+  } catch (const std::exception& e) {
+    error->type = ntc_unknown_error;
+    t_msg = e.what();
+    error->message = &t_msg[0];
+  } catch (...) {
+    error->type = ntc_unknown_error;
+    t_msg = "unknown error";
+    error->message = &t_msg[0];
+  }
+  return decltype(fn())();
+}
+
+}  // namespace ntcx
+
+struct ntc_encoder_t {
+  ntcx::Encoder e;
+};
+struct ntc_decoder_t {
+  ntcx::Decoder d;
+};
+
+extern "C" {
+
+// ----------------------------------------------------------------------------- data ----
+ntc_data_t* ntc_new_data(uint16_t size) noexcept
+{
+  auto* d = new (std::nothrow) ntc_data_t;
+  if (!d) return nullptr;
+  try { d->v.assign(size, 0); } catch (...) { delete d; return nullptr; }
+  return d;
+}
+ntc_data_t* ntc_new_data_from(const char* src, uint16_t size) noexcept
+{
+  auto* d = ntc_new_data(size);
+  if (d && size) std::memcpy(d->v.data(), src, size);
+  return d;
+}
+void ntc_delete_data(ntc_data_t* d) noexcept { delete d; }
+char* ntc_data_buffer(ntc_data_t* d) noexcept { return reinterpret_cast<char*>(d->v.data()); }
+uint16_t ntc_data_get_size(const ntc_data_t* d) noexcept { return static_cast<uint16_t>(d->v.size()); }
+void ntc_data_resize(ntc_data_t* d, uint16_t n, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { d->v.resize(n, 0); }, error);
+}
+
+// --------------------------------------------------------------------------- packet ----
+ntc_packet_t* ntc_new_packet(uint16_t size) noexcept
+{
+  try { return new ntc_packet_t(size); } catch (...) { return nullptr; }
+}
+ntc_packet_t* ntc_new_packet_from(const char* src, uint16_t size) noexcept
+{
+  auto* p = ntc_new_packet(size);
+  if (p && size) std::memcpy(p->data(), src, size);
+  return p;
+}
+void ntc_delete_packet(ntc_packet_t* p) noexcept { delete p; }
+char* ntc_packet_buffer(ntc_packet_t* p) noexcept { return reinterpret_cast<char*>(p->data()); }
+uint16_t ntc_packet_get_size(const ntc_packet_t* p) noexcept { return static_cast<uint16_t>(p->size()); }
+void ntc_packet_resize(ntc_packet_t* p, uint16_t n, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { p->v.resize(n + ntc_packet_t::shift, 0); }, error);
+}
+
+// -------------------------------------------------------------------------- encoder ----
+ntc_encoder_t* ntc_new_encoder(uint8_t galois_field_size, ntc_packet_handler handler) noexcept
+{
+  try { return new ntc_encoder_t{ntcx::Encoder(galois_field_size, handler)}; } catch (...) { return nullptr; }
+}
+void ntc_delete_encoder(ntc_encoder_t* enc) noexcept { delete enc; }
+void ntc_encoder_add_data(ntc_encoder_t* enc, ntc_data_t* data, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] {
+    ntcx::bytes v = std::move(data->v);
+    data->v = ntcx::bytes();                       // moved-from: empty until resized
+    enc->e.add_data(std::move(v));
+  }, error);
+}
+size_t ntc_encoder_add_packet(ntc_encoder_t* enc, ntc_packet_t* packet, ntc_error* error) noexcept
+{
+  return ntcx::guarded([&] {
+    ntcx::bytes v = std::move(packet->v);
+    packet->v = ntcx::bytes(ntc_packet_t::shift, 0);
+    const size_t n = v.size() - ntc_packet_t::shift;
+    return enc->e.add_packet(v.data() + ntc_packet_t::shift, n);
+  }, error);
+}
+void ntc_encoder_generate_repair(ntc_encoder_t* enc, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { enc->e.generate_repair(); }, error);
+}
+size_t ntc_encoder_window(ntc_encoder_t* enc) noexcept { return enc->e.window(); }
+void ntc_encoder_set_code_type(ntc_encoder_t* enc, ntc_code_type t) noexcept { enc->e.set_systematic(t == ntc_systematic_yes); }
+void ntc_encoder_set_rate(ntc_encoder_t* enc, size_t rate) noexcept { enc->e.set_rate(rate); }
+void ntc_encoder_set_window_size(ntc_encoder_t* enc, size_t size) noexcept { enc->e.set_window_size(size); }
+void ntc_encoder_set_adaptive(ntc_encoder_t* enc, bool a) noexcept { enc->e.set_adaptive(a); }
+
+// -------------------------------------------------------------------------- decoder ----
+ntc_decoder_t* ntc_new_decoder(uint8_t galois_field_size, ntc_ordering_type order,
+                               ntc_packet_handler ph, ntc_data_handler dh) noexcept
+{
+  try {
+    return new ntc_decoder_t{ntcx::Decoder(galois_field_size, order == ntc_in_order_yes, ph, dh)};
+  } catch (...) {
+    return nullptr;
+  }
+}
+void ntc_delete_decoder(ntc_decoder_t* dec) noexcept { delete dec; }
+size_t ntc_decoder_add_packet(ntc_decoder_t* dec, ntc_packet_t* packet, ntc_error* error) noexcept
+{
+  return ntcx::guarded([&] {
+    ntcx::bytes v = std::move(packet->v);
+    packet->v = ntcx::bytes(ntc_packet_t::shift, 0);
+    const size_t n = v.size() - ntc_packet_t::shift;
+    return dec->d.add_packet(v.data() + ntc_packet_t::shift, n);
+  }, error);
+}
+void ntc_decoder_generate_ack(ntc_decoder_t* dec, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { dec->d.generate_ack(); }, error);
+}
+void ntc_decoder_set_ack_period(ntc_decoder_t* dec, size_t period) noexcept { dec->d.set_ack_period(period); }
+void ntc_decoder_set_ack_nb_packets(ntc_decoder_t* dec, uint16_t nb) noexcept { dec->d.set_ack_nb_packets(nb); }
+
+// ---------------------------------------------------------------- extensions (ext.h) ----
+size_t ntc_encoder_counter(const ntc_encoder_t* enc, int which) noexcept { return enc->e.counter(which); }
+size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) noexcept { return dec->d.counter(which); }
+
+}  // extern "C"

@@ -1021,6 +1021,30 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
 }
 
+uint32_t ntc_gf256_coef_pitch(uint32_t rows) { return tile_rp(rows); }
+
+int ntc_gf256_combine_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t rows,
+                            uint32_t stride, const uint8_t* in, const uint8_t* coef, uint8_t* out,
+                            void* stream)
+{
+  if (!e || !in || !coef || !out) return fail(NTC_GPU_EINVAL, "NULL argument");
+  int rc = check_shape(G, k, rows, stride);
+  if (rc) return rc;
+  if (rows == 0) return NTC_GPU_OK;
+  const int D = pick_d(stride);
+  MacArgs a{};
+  a.G = G; a.k = k; a.rows = rows; a.stride = stride;
+  a.nrowchunks = (rows + 31) / 32;
+  a.ncolchunks = (stride + 256u * D - 1) / (256u * D);
+  a.in0 = in; a.out = out; a.coef = coef; a.rp = tile_rp(rows);
+  const uint64_t tasks = static_cast<uint64_t>(G) * a.nrowchunks * a.ncolchunks;
+  const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
+  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
+  hipLaunchKernelGGL(pick_kernel(false, D), dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a);
+  return hip_check(hipGetLastError(), "combine launch");
+}
+
 int ntc_gf256_region_multiply(ntc_gf256_engine* e, const uint8_t* src, uint8_t* dst, size_t len,
                               uint8_t c, int add, void* stream)
 {

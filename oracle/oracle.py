@@ -268,3 +268,24 @@ class Decoder:
         if name in Decoder.COUNTERS:
             return lib().or_decoder_counter(self.h, Decoder.COUNTERS.index(name))
         raise AttributeError(name)
+
+
+# --------------------------------------------------------------------------- loss models
+class _BurstS(C.Structure):
+    _fields_ = [("state", C.c_uint32), ("bad", C.c_int), ("good_th", C.c_uint),
+                ("bad_th", C.c_uint)]
+
+
+class Burst:
+    """tools/loss/burst.hh (libstdc++ minstd_rand0 + uniform_int_distribution{1,100})."""
+
+    def __init__(self, good: int, bad: int):
+        self.s = _BurstS()
+        L = lib()
+        L.or_burst_init.argtypes = [C.POINTER(_BurstS), C.c_uint, C.c_uint]
+        L.or_burst_next.argtypes = [C.POINTER(_BurstS)]
+        L.or_burst_next.restype = C.c_int
+        L.or_burst_init(C.byref(self.s), good, bad)
+
+    def __call__(self) -> bool:
+        return bool(lib().or_burst_next(C.byref(self.s)))

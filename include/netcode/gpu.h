@@ -66,6 +66,13 @@ typedef struct ntc_gf256_engine ntc_gf256_engine;
 int  ntc_gf256_engine_create(int device, ntc_gf256_engine** out);
 void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
 
+/* Region-MAC formulation (tuning and A/B testing; results are identical).  AUTO picks the
+ * bit-sliced XOR kernel when the stride fills >= 70 % of its 2 KiB wave span (stride % 32 == 0),
+ * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice environment variable overrides
+ * AUTO process-wide. */
+enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2 };
+int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);
+
 /* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture). */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
 

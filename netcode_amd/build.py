@@ -12,6 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# Uniform (scalar) branches stay real branches instead of being flattened by the CFG
+# structurizer: the bit-sliced MAC dispatches on wave-uniform coefficient nibbles.
+DEVFLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions"]
 
 TARGETS = {
     # GF(2^8) engine: kernels + batched C ABI (include/netcode/gpu.h)
@@ -41,7 +44,7 @@ def build(force: bool = False, verbose: bool = True) -> list[str]:
         if not force and not _stale(out_p, srcs_p):
             built.append(out_p)
             continue
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared"] + DEVFLAGS + [
                "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out_p + ".tmp"] + srcs_p + link
         if verbose:
             print("[netcode_amd.build]", " ".join(cmd), file=sys.stderr)

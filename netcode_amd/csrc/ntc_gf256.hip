@@ -43,6 +43,12 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
   return d;
 }
 
+// Same op through the compiler builtin: schedulable, no inline-asm hazard padding.
+__device__ __forceinline__ uint32_t bxor3(uint32_t a, uint32_t b, uint32_t c)
+{
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 template <int D> struct RowVec;
@@ -156,6 +162,8 @@ struct MacArgs {
   const uint16_t* out_idx;     // decode: plan_out [G][rp] (destination source slot per row)
   const uint8_t* coef;         // [G][k][rp] coefficient bytes, row-minor
   uint32_t rp;
+  const uint32_t* joff;        // bit-sliced kernel: block offsets [G][k][ntiles][16]
+  uint32_t ntiles;
 };
 
 // ---- hand-scheduled scalar loads -------------------------------------------------------------
@@ -334,6 +342,182 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
     for (int j = 0; j < R; ++j)
       if (static_cast<uint32_t>(j) < nrows) store_row<D>(base + j * stride, acc[j]);
   }
+}
+
+// ---- bit-sliced MAC: jump-chained XOR blocks ---------------------------------------------------
+// A lane owns 32 bytes = 8 dwords.  transpose8 turns them into 8 bit-planes (plane p = bit p of
+// every byte; an involution, so the same code slices and un-slices).  Multiplication by c is then
+// linear over GF(2): c*x = sum_t c_t (alpha^t x), with y_t = alpha^t x built per source by the
+// xtime recurrence (29 distinct planes).  Each (row, coefficient nibble) "site" is a table of 16
+// fixed-size blocks of v_xor/v_bitop3 (gf_bitslice_chain.inc, generated by
+// tools/gen_bitslice_chain.py); a source's 2R sites run as a chain of s_setpc jumps whose block
+// offsets bj_offsets precomputed from the coefficient matrix.  Per (source, row) that is ~20
+// full-rate VALU ops for 32 bytes plus 6 scalar ops, against 24 half-rate v_perm + 12 XOR for
+// the byte-domain kernel.
+#include "gf_bitslice_chain.inc"
+
+__device__ __forceinline__ void swap_blocks(uint32_t& a, uint32_t& b, uint32_t sh, uint32_t mask)
+{
+  const uint32_t t = ((a >> sh) ^ b) & mask;
+  b ^= t;
+  a ^= t << sh;
+}
+
+__device__ __forceinline__ void transpose8(uint32_t* d)
+{
+#pragma unroll
+  for (int i = 0; i < 4; ++i) swap_blocks(d[i], d[i + 4], 4, 0x0F0F0F0Fu);
+#pragma unroll
+  for (int i = 0; i < 8; i += 4) {
+    swap_blocks(d[i], d[i + 2], 2, 0x33333333u);
+    swap_blocks(d[i + 1], d[i + 3], 2, 0x33333333u);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) swap_blocks(d[i], d[i + 1], 1, 0x55555555u);
+}
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// Loads through the constant address space: always scalar (s_load) for a uniform address, with
+// the waits placed by the compiler.  Used for data no kernel in flight writes (offsets, plans).
+template <typename T>
+__device__ __forceinline__ T const_load(const void* p)
+{
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(
+      reinterpret_cast<uintptr_t>(p));
+}
+
+// Block offsets of one (generation, source, row tile): 16 sites = 8 rows x 2 nibbles.
+__global__ __launch_bounds__(256) void bj_offsets(const uint8_t* __restrict__ coef, uint32_t rp,
+                                                  uint32_t ntiles, uint64_t total,
+                                                  uint32_t* __restrict__ joff)
+{
+  const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (idx >= total) return;
+  const uint32_t site = static_cast<uint32_t>(idx & 15u);
+  const uint64_t q = idx >> 4;
+  const uint32_t tile = static_cast<uint32_t>(q % ntiles);
+  const uint64_t gk = q / ntiles;
+  const uint32_t j = tile * 8u + (site >> 1);
+  const uint32_t c = j < rp ? coef[gk * rp + j] : 0u;
+  const uint32_t v = (c >> (4u * (site & 1u))) & 15u;
+  joff[idx] = site * kBjSite + v * kBjBlock;
+}
+
+template <int R, bool DEC>
+__device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
+                                            uint32_t nrows, uint32_t col, bool active)
+{
+  const size_t stride = a.stride;
+  const uint32_t k = a.k;
+  const uint32_t colx = active ? col : 0u;
+  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride + colx;
+  const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride + colx : nullptr;
+  const uint16_t* in = DEC ? a.in_idx + static_cast<size_t>(g) * k : nullptr;
+  const uint32_t jstep = a.ntiles * 16u;
+  const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * 16u;
+  // Offsets and plan entries are loaded with ordinary uniform loads (the compiler turns them into
+  // s_load and places the waits; inline-asm loads raced with compiler copies of their results).
+  // decode: plan_in entry i via the dword holding it (4-byte aligned scalar load, then shift)
+  auto in_word = [&](uint32_t i) -> uint32_t {
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(in + i);
+    return const_load<uint32_t>(reinterpret_cast<const void*>(ad & ~static_cast<uintptr_t>(3))) >>
+           (8u * (ad & 2u));
+  };
+  auto rowptr = [&](uint32_t i, uint32_t w) -> const uint8_t* {
+    if constexpr (DEC) {
+      (void)i;
+      const uint32_t ii = w & 0xFFFFu;
+      return ii < k ? base0 + ii * stride : base1 + (ii - k) * stride;
+    } else {
+      (void)w;
+      return base0 + i * stride;
+    }
+  };
+
+  uint32_t acc[R][8];
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[j][p] = 0;
+
+  uint32_t w0 = 0, wn = 0;
+  if constexpr (DEC) w0 = in_word(0);
+  uint32_t nx[8];
+  {
+    const uint4* q = reinterpret_cast<const uint4*>(rowptr(0, w0));
+    const uint4 v0 = q[0], v1 = q[1];
+    nx[0] = v0.x; nx[1] = v0.y; nx[2] = v0.z; nx[3] = v0.w;
+    nx[4] = v1.x; nx[5] = v1.y; nx[6] = v1.z; nx[7] = v1.w;
+  }
+  u32x16 on = const_load<u32x16>(jrow);
+  if constexpr (DEC) wn = in_word(k > 1 ? 1u : 0u);
+  for (uint32_t i = 0; i < k; ++i) {
+    const u32x16 o = on;
+    const uint32_t w = wn;
+    uint32_t Y[kBjPlanes];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) Y[p] = nx[p];
+    // Prefetch source i+1 (clamped: the last iteration reloads the same row; no branch).
+    const uint32_t i1 = i + 1 < k ? i + 1 : i;
+    {
+      const uint4* q = reinterpret_cast<const uint4*>(rowptr(i1, w));
+      const uint4 v0 = q[0], v1 = q[1];
+      nx[0] = v0.x; nx[1] = v0.y; nx[2] = v0.z; nx[3] = v0.w;
+      nx[4] = v1.x; nx[5] = v1.y; nx[6] = v1.z; nx[7] = v1.w;
+    }
+    on = const_load<u32x16>(jrow + static_cast<size_t>(i1) * jstep);
+    if constexpr (DEC) wn = in_word(i + 2 < k ? i + 2 : i1);
+    transpose8(Y);
+    NTC_BJ_XTIME(Y)
+    uint32_t O[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) O[s] = o[s];
+    if constexpr (R == 8) {
+      asm volatile(NTC_BJ_CHAIN_R8 : NTC_BJ_OUTS_R8(acc) : NTC_BJ_INS_R8(Y, O) : NTC_BJ_CLOBBERS);
+    } else {
+      asm volatile(NTC_BJ_CHAIN_R4 : NTC_BJ_OUTS_R4(acc) : NTC_BJ_INS_R4(Y, O) : NTC_BJ_CLOBBERS);
+    }
+  }
+
+  if (!active) return;
+  const uint32_t row0 = tile * 8u;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (static_cast<uint32_t>(j) >= nrows) continue;
+    transpose8(acc[j]);
+    uint8_t* dst;
+    if constexpr (DEC) {
+      const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
+      dst = a.out + static_cast<size_t>(g) * k * stride + uniform(outs[j]) * stride + col;
+    } else {
+      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride + col;
+    }
+    uint4* q = reinterpret_cast<uint4*>(dst);
+    q[0] = make_uint4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    q[1] = make_uint4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
+  }
+}
+
+// One wave per (generation, 8-row tile, 2 KiB column span).
+template <bool DEC>
+__global__ __launch_bounds__(256) void gf_mac_bj(MacArgs a)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t task = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const uint32_t cc = task % a.ncolchunks;
+  task /= a.ncolchunks;
+  const uint32_t tile = task % a.nrowchunks;
+  const uint32_t g = task / a.nrowchunks;
+  if (g >= a.G) return;
+  const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
+  const uint32_t row0 = tile * 8u;
+  if (row0 >= total) return;
+  const uint32_t nrows = min(8u, total - row0);
+  const uint32_t col = cc * 2048u + lane * 32u;
+  const bool active = col < a.stride;
+  if (nrows > 4) mac_tile_bj<8, DEC>(a, g, tile, nrows, col, active);
+  else mac_tile_bj<4, DEC>(a, g, tile, nrows, col, active);
 }
 
 // Encode (DEC = false): rep[g][rows] = C_g * src[g]; decode (DEC = true): the plan's D_g applied to
@@ -757,6 +941,9 @@ struct ntc_gf256_engine {
   uint8_t* plan_coef = nullptr;
   void* enc_coef = nullptr;
   size_t enc_coef_cap = 0;
+  void* joff = nullptr;        // bit-sliced MAC block offsets
+  size_t joff_cap = 0;
+  int mac_kind = NTC_GF256_MAC_AUTO;
   // geometry of the last plan (decode_apply must match)
   uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
 };
@@ -800,6 +987,59 @@ mac_fn pick_kernel(bool dec, int D)
 {
   if (dec) return D == 4 ? gf_mac<4, true> : D == 2 ? gf_mac<2, true> : gf_mac<1, true>;
   return D == 4 ? gf_mac<4, false> : D == 2 ? gf_mac<2, false> : gf_mac<1, false>;
+}
+
+// MAC formulation for a stride.  The bit-sliced kernel needs 32-byte lanes (stride % 32 == 0) and
+// spans 2 KiB per wave, so short symbols leave lanes idle; measured on MI355X it beats the v_perm
+// kernel (8-byte lanes) once >= ~70 % of its lanes carry data (41 vs 28 T byte-MAC/s at full use).
+// NTC_GF256_MAC=perm|bitslice forces one (A/B experiments).
+bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
+{
+  if (stride % 32 != 0) return false;
+  if (e->mac_kind != NTC_GF256_MAC_AUTO) return e->mac_kind == NTC_GF256_MAC_BITSLICE;
+  static const int forced = [] {
+    const char* s = std::getenv("NTC_GF256_MAC");
+    if (!s) return 0;
+    if (!std::strcmp(s, "perm")) return 1;
+    if (!std::strcmp(s, "bitslice")) return 2;
+    return 0;
+  }();
+  if (forced) return forced == 2;
+  const uint32_t lanes = stride / 32, spans = (stride + 2047) / 2048;
+  return lanes * 100 >= spans * 64 * 70;
+}
+
+int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
+
+// Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
+int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what)
+{
+  mac_fn fn;
+  uint32_t rowtile = 32, span;
+  if (use_bitslice(e, a.stride)) {
+    rowtile = 8;
+    span = 2048;
+    fn = dec ? gf_mac_bj<true> : gf_mac_bj<false>;
+    a.ntiles = (a.rows + 7) / 8;
+    const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 16u;
+    int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
+    if (rc) return rc;
+    a.joff = static_cast<const uint32_t*>(e->joff);
+    hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
+                       a.coef, a.rp, a.ntiles, n, static_cast<uint32_t*>(e->joff));
+    if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
+  } else {
+    const int D = pick_d(a.stride);
+    span = 256u * D;
+    fn = pick_kernel(dec, D);
+  }
+  a.nrowchunks = (a.rows + rowtile - 1) / rowtile;
+  a.ncolchunks = (a.stride + span - 1) / span;
+  const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
+  const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
+  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
+  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, st, a);
+  return hip_check(hipGetLastError(), what);
 }
 
 // Coefficient rows padded to the row tile the MAC kernel reads (4, 8, 16 or a multiple of 32).
@@ -862,7 +1102,9 @@ const char* ntc_gf256_last_error(void) { return g_err.c_str(); }
 
 const char* ntc_gf256_build_info(void)
 {
-  return "libntc_gf256 gfx950: v_perm_b32 3/3/2 split + v_bitop3 XOR, R in {4,8,16,32}, D in {1,2,4}";
+  return "libntc_gf256 gfx950: bit-sliced jump-chained XOR MAC (32 B lanes, 8-row tiles) for strides "
+         "filling >= 70 % of a 2 KiB wave span; v_perm_b32 3/3/2 split MAC (R in {4,8,16,32}, D in "
+         "{1,2,4}) otherwise";
 }
 
 uint32_t ntc_gf256_coefficient(uint32_t repair_id, uint32_t src_id) { return coefficient(repair_id, src_id); }
@@ -906,7 +1148,16 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_out);
   (void)hipFree(e->plan_coef);
   (void)hipFree(e->enc_coef);
+  (void)hipFree(e->joff);
   delete e;
+}
+
+int ntc_gf256_set_mac_kind(ntc_gf256_engine* e, int kind)
+{
+  if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
+  if (kind < NTC_GF256_MAC_AUTO || kind > NTC_GF256_MAC_BITSLICE) return fail(NTC_GPU_EINVAL, "unknown MAC kind");
+  e->mac_kind = kind;
+  return NTC_GPU_OK;
 }
 
 int ntc_gf256_reserve(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r)
@@ -939,17 +1190,10 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   p.rep_len = rep_len;
   hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
   if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
-  const int D = pick_d(stride);
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
-  a.nrowchunks = (r + 31) / 32;
-  a.ncolchunks = (stride + 256u * D - 1) / (256u * D);
   a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
-  const uint64_t tasks = static_cast<uint64_t>(G) * a.nrowchunks * a.ncolchunks;
-  const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
-  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
-  hipLaunchKernelGGL(pick_kernel(false, D), dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, st, a);
-  return hip_check(hipGetLastError(), "encode_mac launch");
+  return launch_mac(e, false, a, st, "encode_mac launch");
 }
 
 int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -991,20 +1235,12 @@ int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   if (G != e->last_G || k != e->last_k || r != e->last_r)
     return fail(NTC_GPU_EINVAL, "decode_apply geometry differs from the last decode_plan");
   if (r == 0) return NTC_GPU_OK;
-  const int D = pick_d(stride);
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
-  a.nrowchunks = (r + 31) / 32;
-  a.ncolchunks = (stride + 256u * D - 1) / (256u * D);
   a.in0 = src; a.in1 = rep; a.out = src;
   a.rows_per_gen = e->plan_m; a.in_idx = e->plan_in; a.out_idx = e->plan_out;
   a.coef = e->plan_coef; a.rp = e->last_rp;
-  const uint64_t tasks = static_cast<uint64_t>(G) * a.nrowchunks * a.ncolchunks;
-  const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
-  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
-  hipLaunchKernelGGL(pick_kernel(true, D), dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), a);
-  return hip_check(hipGetLastError(), "decode_mac launch");
+  return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch");
 }
 
 int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -1031,18 +1267,10 @@ int ntc_gf256_combine_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_
   int rc = check_shape(G, k, rows, stride);
   if (rc) return rc;
   if (rows == 0) return NTC_GPU_OK;
-  const int D = pick_d(stride);
   MacArgs a{};
   a.G = G; a.k = k; a.rows = rows; a.stride = stride;
-  a.nrowchunks = (rows + 31) / 32;
-  a.ncolchunks = (stride + 256u * D - 1) / (256u * D);
   a.in0 = in; a.out = out; a.coef = coef; a.rp = tile_rp(rows);
-  const uint64_t tasks = static_cast<uint64_t>(G) * a.nrowchunks * a.ncolchunks;
-  const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
-  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
-  hipLaunchKernelGGL(pick_kernel(false, D), dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), a);
-  return hip_check(hipGetLastError(), "combine launch");
+  return launch_mac(e, false, a, static_cast<hipStream_t>(stream), "combine launch");
 }
 
 int ntc_gf256_region_multiply(ntc_gf256_engine* e, const uint8_t* src, uint8_t* dst, size_t len,

@@ -94,6 +94,13 @@ class Engine:
     def handle(self):
         return self._h
 
+    MAC_KINDS = {"auto": 0, "perm": 1, "bitslice": 2}
+
+    def set_mac_kind(self, kind: str = "auto"):
+        """Select the region-MAC formulation (ntc_gf256_set_mac_kind); results are identical."""
+        _native.check(self._L.ntc_gf256_set_mac_kind(self._h, Engine.MAC_KINDS[kind]),
+                      "ntc_gf256_set_mac_kind")
+
     def reserve(self, G: int, k: int, r: int):
         _native.check(self._L.ntc_gf256_reserve(self._h, G, k, r), "ntc_gf256_reserve")
 

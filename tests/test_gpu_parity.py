@@ -50,6 +50,16 @@ def gpu_decode(d, lost, llen, smask, rep, rsz, rmask, sid=None, rid=None):
     return host(s_t), host(l_t, np.uint16), status_to_numpy(st)
 
 
+@pytest.fixture(params=["auto", "perm", "bitslice"])
+def mac(request, gpu):
+    """Run a parity test under each region-MAC formulation (ntc_gf256_set_mac_kind)."""
+    from netcode_amd.engine import Engine
+    eng = Engine.get(gpu)
+    eng.set_mac_kind(request.param)
+    yield request.param
+    eng.set_mac_kind("auto")
+
+
 def test_region_multiply(gpu, oracle):
     import torch
     from netcode_amd import GaloisField
@@ -79,6 +89,7 @@ ENCODE_CASES = [
     (4, 33, 40, 256, 256, False, "offset"),           # odd k, r > 32 (two row chunks)
     (3, 1, 1, 16, 16, True, "default"),               # minimum shape
     (2, 7, 3, 4096, 4112, True, "offset"),            # stride not a multiple of the wave span
+    (5, 9, 12, 2080, 2080, True, "offset"),           # 2 KiB spans + a 1-lane tail; 8+4 row tiles
 ]
 
 
@@ -93,7 +104,7 @@ def _ids(mode, G, k, r):
 
 
 @pytest.mark.parametrize("G,k,r,S,stride,ragged,ids", ENCODE_CASES)
-def test_encode_parity(gpu, oracle, G, k, r, S, stride, ragged, ids):
+def test_encode_parity(gpu, mac, oracle, G, k, r, S, stride, ragged, ids):
     src, lens = make_sources(G, k, S, stride, seed=G * 1000 + k + r, ragged=ragged)
     sid, rid = _ids(ids, G, k, r)
     rep, rsz, rlen = gpu_encode(gpu, src, lens, k, r, sid, rid)
@@ -104,7 +115,7 @@ def test_encode_parity(gpu, oracle, G, k, r, S, stride, ragged, ids):
 
 
 @pytest.mark.parametrize("name", ["gen_k16_r4_loss25", "gen_k32_r8_ragged"])
-def test_decode_golden_fixtures(gpu, name):
+def test_decode_golden_fixtures(gpu, mac, name):
     z = np.load(os.path.join(HERE, "golden", name + ".npz"))
     k, r = z["src"].shape[1], z["rep"].shape[1]
     rep, rsz, _ = gpu_encode(gpu, z["src"], z["src_len"], k, r, z["sid_base"], z["rid_base"])
@@ -130,11 +141,13 @@ DECODE_CASES = [
     (40, 32, 8, 512, 512, "exact", 1, True),          # single loss -> peeling path
     (40, 32, 8, 512, 512, "exact", 0, False),         # nothing missing -> useless repairs
     (10, 48, 40, 256, 256, "exact", 40, False),       # m = r = 40 (> one row tile)
+    (9, 33, 12, 2080, 2080, "exact", 12, True),       # odd k (unaligned plan rows), 8+4 row tiles
+    (30, 7, 5, 4096, 4096, "iid", 0.3, False),        # tiny k, mixed outcomes
 ]
 
 
 @pytest.mark.parametrize("G,k,r,S,stride,kind,param,ragged", DECODE_CASES)
-def test_decode_parity(gpu, oracle, G, k, r, S, stride, kind, param, ragged):
+def test_decode_parity(gpu, mac, oracle, G, k, r, S, stride, kind, param, ragged):
     seed = G * 7 + k * 3 + r
     src, lens = make_sources(G, k, S, stride, seed=seed, ragged=ragged)
     sid = (np.arange(G) * k + 3).astype(np.uint32)

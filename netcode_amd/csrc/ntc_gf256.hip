@@ -387,44 +387,97 @@ __device__ __forceinline__ T const_load(const void* p)
       reinterpret_cast<uintptr_t>(p));
 }
 
-// Block offsets of one (generation, source, row tile): 16 sites = 8 rows x 2 nibbles.
+// Block offsets of one (generation, source, row tile): 2*RT sites = RT rows x 2 nibbles.
 __global__ __launch_bounds__(256) void bj_offsets(const uint8_t* __restrict__ coef, uint32_t rp,
-                                                  uint32_t ntiles, uint64_t total,
+                                                  uint32_t rt, uint32_t ntiles, uint64_t total,
                                                   uint32_t* __restrict__ joff)
 {
   const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
   if (idx >= total) return;
-  const uint32_t site = static_cast<uint32_t>(idx & 15u);
-  const uint64_t q = idx >> 4;
+  const uint32_t nsites = 2u * rt;
+  const uint32_t site = static_cast<uint32_t>(idx % nsites);
+  const uint64_t q = idx / nsites;
   const uint32_t tile = static_cast<uint32_t>(q % ntiles);
   const uint64_t gk = q / ntiles;
-  const uint32_t j = tile * 8u + (site >> 1);
+  const uint32_t j = tile * rt + (site >> 1);
   const uint32_t c = j < rp ? coef[gk * rp + j] : 0u;
   const uint32_t v = (c >> (4u * (site & 1u))) & 15u;
-  joff[idx] = site * kBjSite + v * kBjBlock;
+  joff[idx] = site * kBjSite + kBjVo[v];
 }
 
-template <int R, bool DEC>
+// Source staging: every wave streams its sources through a private ring of kBjRing LDS slots with
+// LDS-DMA (global_load_lds_dwordx4), kBjRing-1 sources ahead, so HBM latency hides behind ~3
+// chain iterations without holding VGPRs.  A lane owns two 16-byte pieces of the 2 KiB column
+// span -- bytes [16*lane, +16) and [1024 + 16*lane, +16) -- so each DMA and each store is one
+// contiguous KiB per wave, and a half is valid whenever its 16 bytes lie inside the stride.
+constexpr int kBjRing = 4;
+constexpr uint32_t kBjSlot = 2048;
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p)
+{
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(
+          reinterpret_cast<uintptr_t>(p))));
+}
+
+// DMA one source's two 16-byte pieces per lane into LDS slot `slot` (wave-uniform byte address).
+// M0 is compiler-reserved: saved and restored inside the statement (cdna_hip_programming.md).
+__device__ __forceinline__ void dma_source(const uint8_t* p0, const uint8_t* p1, uint32_t slot)
+{
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\t"
+               "s_mov_b32 m0, %3\n\t"
+               "s_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\t"
+               "s_add_u32 m0, %3, 0x400\n\t"
+               "s_nop 0\n\t"
+               "global_load_lds_dwordx4 %2, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(p0), "v"(p1), "s"(slot) : "memory", "scc");
+}
+
+// Wait for the DMA of the oldest in-flight source (the 2*(kBjRing-2) younger DMAs may stay in
+// flight), then read this lane's 32 bytes of it.  Loads and waits in one statement: the compiler
+// never sees the destination registers before the data has landed.
+__device__ __forceinline__ void ring_read(uint32_t laddr, uint32_t (&y)[kBjPlanes])
+{
+  u32x4 q0, q1;
+  asm volatile("s_waitcnt vmcnt(%3)\n\t"
+               "ds_read_b128 %0, %2\n\t"
+               "ds_read_b128 %1, %2 offset:1024\n\t"
+               "s_waitcnt lgkmcnt(0)"
+               : "=&v"(q0), "=&v"(q1) : "v"(laddr), "i"(2 * (kBjRing - 2)) : "memory");
+  y[0] = q0[0]; y[1] = q0[1]; y[2] = q0[2]; y[3] = q0[3];
+  y[4] = q1[0]; y[5] = q1[1]; y[6] = q1[2]; y[7] = q1[3];
+}
+
+// ABL != 0: timing ablations of the encode kernel (NTC_GF256_BJ_ABLATE; results are wrong):
+// 1 no transpose, 2 no xtime, 4 straight-line stand-in for the chain, 8 no chain.
+template <int R, int RT, bool DEC, int ABL = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
-                                            uint32_t nrows, uint32_t col, bool active)
+                                            uint32_t nrows, uint32_t cc, uint32_t lane,
+                                            uint32_t ring)
 {
   const size_t stride = a.stride;
   const uint32_t k = a.k;
-  const uint32_t colx = active ? col : 0u;
-  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride + colx;
-  const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride + colx : nullptr;
+  const uint32_t c0 = cc * 2048u + lane * 16u, c1 = c0 + 1024u;
+  const bool v0 = c0 < stride, v1 = c1 < stride;      // stride % 16 == 0: whole pieces
+  const uint32_t x0 = v0 ? c0 : 0u, x1 = v1 ? c1 : 0u;  // invalid pieces read column 0 (unused)
+  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
+  const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
   const uint16_t* in = DEC ? a.in_idx + static_cast<size_t>(g) * k : nullptr;
-  const uint32_t jstep = a.ntiles * 16u;
-  const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * 16u;
-  // Offsets and plan entries are loaded with ordinary uniform loads (the compiler turns them into
-  // s_load and places the waits; inline-asm loads raced with compiler copies of their results).
+  const uint32_t jstep = a.ntiles * 2u * RT;
+  const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * (2u * RT);
+  constexpr int NJ = R == 16 ? 2 : 1;     // u32x16 offset vectors per source
+  // Offsets and plan entries are loaded with ordinary uniform loads through the constant address
+  // space (s_load, waits placed by the compiler).
   // decode: plan_in entry i via the dword holding it (4-byte aligned scalar load, then shift)
   auto in_word = [&](uint32_t i) -> uint32_t {
     const uintptr_t ad = reinterpret_cast<uintptr_t>(in + i);
     return const_load<uint32_t>(reinterpret_cast<const void*>(ad & ~static_cast<uintptr_t>(3))) >>
            (8u * (ad & 2u));
   };
-  auto rowptr = [&](uint32_t i, uint32_t w) -> const uint8_t* {
+  auto row_of = [&](uint32_t i, uint32_t w) -> const uint8_t* {
     if constexpr (DEC) {
       (void)i;
       const uint32_t ii = w & 0xFFFFu;
@@ -434,6 +487,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
       return base0 + i * stride;
     }
   };
+  auto clampk = [&](uint32_t i) -> uint32_t { return i < k ? i : k - 1; };
 
   uint32_t acc[R][8];
 #pragma unroll
@@ -441,47 +495,71 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[j][p] = 0;
 
-  uint32_t w0 = 0, wn = 0;
-  if constexpr (DEC) w0 = in_word(0);
-  uint32_t nx[8];
-  {
-    const uint4* q = reinterpret_cast<const uint4*>(rowptr(0, w0));
-    const uint4 v0 = q[0], v1 = q[1];
-    nx[0] = v0.x; nx[1] = v0.y; nx[2] = v0.z; nx[3] = v0.w;
-    nx[4] = v1.x; nx[5] = v1.y; nx[6] = v1.z; nx[7] = v1.w;
+  // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait count is constant).
+#pragma unroll
+  for (int q = 0; q < kBjRing - 1; ++q) {
+    const uint32_t iq = clampk(q);
+    const uint8_t* row = row_of(iq, DEC ? in_word(iq) : 0u);
+    dma_source(row + x0, row + x1, ring + q * kBjSlot);
   }
-  u32x16 on = const_load<u32x16>(jrow);
-  if constexpr (DEC) wn = in_word(k > 1 ? 1u : 0u);
+  uint32_t wn = 0;
+  if constexpr (DEC) wn = in_word(clampk(kBjRing - 1));
+  u32x16 on[NJ];
+#pragma unroll
+  for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + 16 * h);
+  const uint32_t lane_off = lane * 16u;
   for (uint32_t i = 0; i < k; ++i) {
-    const u32x16 o = on;
-    const uint32_t w = wn;
+    u32x16 o[NJ];
+#pragma unroll
+    for (int h = 0; h < NJ; ++h) o[h] = on[h];
     uint32_t Y[kBjPlanes];
-#pragma unroll
-    for (int p = 0; p < 8; ++p) Y[p] = nx[p];
-    // Prefetch source i+1 (clamped: the last iteration reloads the same row; no branch).
-    const uint32_t i1 = i + 1 < k ? i + 1 : i;
-    {
-      const uint4* q = reinterpret_cast<const uint4*>(rowptr(i1, w));
-      const uint4 v0 = q[0], v1 = q[1];
-      nx[0] = v0.x; nx[1] = v0.y; nx[2] = v0.z; nx[3] = v0.w;
-      nx[4] = v1.x; nx[5] = v1.y; nx[6] = v1.z; nx[7] = v1.w;
+    ring_read(ring + (i % kBjRing) * kBjSlot + lane_off, Y);
+    {   // refill the slot read last iteration with source i + kBjRing - 1
+      const uint32_t iq = clampk(i + kBjRing - 1);
+      const uint8_t* row = row_of(iq, wn);
+      dma_source(row + x0, row + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
+      if constexpr (DEC) wn = in_word(clampk(i + kBjRing));
     }
-    on = const_load<u32x16>(jrow + static_cast<size_t>(i1) * jstep);
-    if constexpr (DEC) wn = in_word(i + 2 < k ? i + 2 : i1);
-    transpose8(Y);
-    NTC_BJ_XTIME(Y)
-    uint32_t O[16];
+    const uint32_t i1 = clampk(i + 1);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) O[s] = o[s];
-    if constexpr (R == 8) {
+    for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + static_cast<size_t>(i1) * jstep + 16 * h);
+    if constexpr (!(ABL & 1)) transpose8(Y);
+    if constexpr (!(ABL & 2)) {
+      NTC_BJ_XTIME(Y)
+    } else {
+#pragma unroll
+      for (int n = 8; n < kBjPlanes; ++n) Y[n] = Y[n & 7] + n;
+    }
+    uint32_t O[16 * NJ];
+#pragma unroll
+    for (int s = 0; s < 16 * NJ; ++s) O[s] = o[s >> 4][s & 15];
+    if constexpr ((ABL & 4) != 0) {   // straight-line stand-in for the chain: 16 VALU per row
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          acc[j][p] = bxor3(acc[j][p], Y[(j + p) % 29], Y[(j + 2 * p + 3) % 29]);
+          acc[j][p] = bxor3(acc[j][p], Y[(3 * j + p + 7) % 29], O[(j + p) & 15]);
+        }
+      continue;
+    }
+    if constexpr ((ABL & 8) != 0) {   // no chain: keep the planes alive with one row's XORs
+#pragma unroll
+      for (int p = 0; p < 8; ++p) acc[0][p] = bxor3(acc[0][p], Y[p + 8], Y[p + 16]) ^ O[p];
+      continue;
+    }
+    if constexpr (R == 16) {
+      asm volatile(NTC_BJ_CHAIN_R16 : NTC_BJ_OUTS_R16(acc) : NTC_BJ_INS_R16(Y, O) : NTC_BJ_CLOBBERS);
+    } else if constexpr (R == 8) {
       asm volatile(NTC_BJ_CHAIN_R8 : NTC_BJ_OUTS_R8(acc) : NTC_BJ_INS_R8(Y, O) : NTC_BJ_CLOBBERS);
     } else {
       asm volatile(NTC_BJ_CHAIN_R4 : NTC_BJ_OUTS_R4(acc) : NTC_BJ_INS_R4(Y, O) : NTC_BJ_CLOBBERS);
     }
   }
+  // Drain the clamped trailing DMAs before the wave's LDS can be handed to another block.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if (!active) return;
-  const uint32_t row0 = tile * 8u;
+  const uint32_t row0 = tile * RT;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     if (static_cast<uint32_t>(j) >= nrows) continue;
@@ -489,35 +567,45 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     uint8_t* dst;
     if constexpr (DEC) {
       const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
-      dst = a.out + static_cast<size_t>(g) * k * stride + uniform(outs[j]) * stride + col;
+      dst = a.out + static_cast<size_t>(g) * k * stride + uniform(outs[j]) * stride;
     } else {
-      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride + col;
+      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
     }
-    uint4* q = reinterpret_cast<uint4*>(dst);
-    q[0] = make_uint4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-    q[1] = make_uint4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
+    if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    if (v1) *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
   }
 }
 
-// One wave per (generation, 8-row tile, 2 KiB column span).
-template <bool DEC>
+// One wave per (generation, RT-row tile, 2 KiB column span).  Blocks are renumbered so that each
+// XCD (block b runs on XCD b % 8) owns a contiguous range of tasks: the row tiles of one
+// generation then share that XCD's L2 instead of each pulling the sources from HBM.
+template <int RT, bool DEC, int ABL = 0>
 __global__ __launch_bounds__(256) void gf_mac_bj(MacArgs a)
 {
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kWaves * kBjRing * kBjSlot];
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t task = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const uint32_t nb = gridDim.x;                       // a multiple of 8 (launch_mac)
+  const uint32_t b = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+  uint32_t task = uniform(b * kWaves + wave);
   const uint32_t cc = task % a.ncolchunks;
   task /= a.ncolchunks;
   const uint32_t tile = task % a.nrowchunks;
   const uint32_t g = task / a.nrowchunks;
   if (g >= a.G) return;
   const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
-  const uint32_t row0 = tile * 8u;
+  const uint32_t row0 = tile * RT;
   if (row0 >= total) return;
-  const uint32_t nrows = min(8u, total - row0);
-  const uint32_t col = cc * 2048u + lane * 32u;
-  const bool active = col < a.stride;
-  if (nrows > 4) mac_tile_bj<8, DEC>(a, g, tile, nrows, col, active);
-  else mac_tile_bj<4, DEC>(a, g, tile, nrows, col, active);
+  const uint32_t nrows = min(static_cast<uint32_t>(RT), total - row0);
+  const uint32_t ring = lds_addr(s_ring) + wave * (kBjRing * kBjSlot);
+  if constexpr (RT == 16) {
+    if (nrows > 8) {
+      mac_tile_bj<16, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring);
+      return;
+    }
+  }
+  if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring);
+  else mac_tile_bj<4, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring);
 }
 
 // Encode (DEC = false): rep[g][rows] = C_g * src[g]; decode (DEC = true): the plan's D_g applied to
@@ -989,13 +1077,13 @@ mac_fn pick_kernel(bool dec, int D)
   return D == 4 ? gf_mac<4, false> : D == 2 ? gf_mac<2, false> : gf_mac<1, false>;
 }
 
-// MAC formulation for a stride.  The bit-sliced kernel needs 32-byte lanes (stride % 32 == 0) and
-// spans 2 KiB per wave, so short symbols leave lanes idle; measured on MI355X it beats the v_perm
+// MAC formulation for a stride.  The bit-sliced kernel spans 2 KiB per wave (two 16-byte pieces per
+// lane), so short symbols leave lanes idle; measured on MI355X it beats the v_perm
 // kernel (8-byte lanes) once >= ~70 % of its lanes carry data (41 vs 28 T byte-MAC/s at full use).
 // NTC_GF256_MAC=perm|bitslice forces one (A/B experiments).
 bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
 {
-  if (stride % 32 != 0) return false;
+  if (stride % 16 != 0) return false;
   if (e->mac_kind != NTC_GF256_MAC_AUTO) return e->mac_kind == NTC_GF256_MAC_BITSLICE;
   static const int forced = [] {
     const char* s = std::getenv("NTC_GF256_MAC");
@@ -1005,8 +1093,8 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
     return 0;
   }();
   if (forced) return forced == 2;
-  const uint32_t lanes = stride / 32, spans = (stride + 2047) / 2048;
-  return lanes * 100 >= spans * 64 * 70;
+  const uint32_t pieces = stride / 16, spans = (stride + 2047) / 2048;   // 16-B pieces per span: 128
+  return pieces * 100 >= spans * 128 * 70;
 }
 
 int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
@@ -1016,27 +1104,50 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
 {
   mac_fn fn;
   uint32_t rowtile = 32, span;
+  uint64_t blk_align = 1;
   if (use_bitslice(e, a.stride)) {
-    rowtile = 8;
+    static const uint32_t rt = [] {
+      const char* v = std::getenv("NTC_GF256_BJ_ROWS");      // 8 | 16 (tuning experiments)
+      return (v && std::atoi(v) == 16) ? 16u : 8u;
+    }();
+    rowtile = rt;
     span = 2048;
-    fn = dec ? gf_mac_bj<true> : gf_mac_bj<false>;
-    a.ntiles = (a.rows + 7) / 8;
-    const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 16u;
+    blk_align = 8;
+    fn = rt == 16 ? (dec ? gf_mac_bj<16, true> : gf_mac_bj<16, false>)
+                  : (dec ? gf_mac_bj<8, true> : gf_mac_bj<8, false>);
+    a.ntiles = (a.rows + rt - 1) / rt;
+    const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 2u * rt;
     int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
     if (rc) return rc;
     a.joff = static_cast<const uint32_t*>(e->joff);
     hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
-                       a.coef, a.rp, a.ntiles, n, static_cast<uint32_t*>(e->joff));
+                       a.coef, a.rp, rt, a.ntiles, n, static_cast<uint32_t*>(e->joff));
     if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
   } else {
     const int D = pick_d(a.stride);
     span = 256u * D;
     fn = pick_kernel(dec, D);
   }
+  static const int ablate = [] {
+    const char* v = std::getenv("NTC_GF256_BJ_ABLATE");
+    return v ? std::atoi(v) : 0;
+  }();
+  if (ablate && fn == gf_mac_bj<8, false>) {
+    switch (ablate) {
+      case 1: fn = gf_mac_bj<8, false, 1>; break;
+      case 2: fn = gf_mac_bj<8, false, 2>; break;
+      case 3: fn = gf_mac_bj<8, false, 3>; break;
+      case 4: fn = gf_mac_bj<8, false, 4>; break;
+      case 8: fn = gf_mac_bj<8, false, 8>; break;
+      case 11: fn = gf_mac_bj<8, false, 11>; break;
+
+      default: break;
+    }
+  }
   a.nrowchunks = (a.rows + rowtile - 1) / rowtile;
   a.ncolchunks = (a.stride + span - 1) / span;
   const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
-  const uint64_t blocks = (tasks + kWaves - 1) / kWaves;
+  const uint64_t blocks = ((tasks + kWaves - 1) / kWaves + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, st, a);
   return hip_check(hipGetLastError(), what);

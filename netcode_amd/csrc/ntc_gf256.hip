@@ -436,17 +436,20 @@ __device__ __forceinline__ void dma_source(const uint8_t* p0, const uint8_t* p1,
                : "=&s"(keep) : "v"(p0), "v"(p1), "s"(slot) : "memory", "scc");
 }
 
-// Wait for the DMA of the oldest in-flight source (the 2*(kBjRing-2) younger DMAs may stay in
-// flight), then read this lane's 32 bytes of it.  Loads and waits in one statement: the compiler
-// never sees the destination registers before the data has landed.
-__device__ __forceinline__ void ring_read(uint32_t laddr, uint32_t (&y)[kBjPlanes])
+// Wait until at most N of this wave's vector-memory operations (LDS-DMA included) are in flight.
+// The "memory" clobber keeps the compiler's LDS reads of the slot below the wait.
+template <int N>
+__device__ __forceinline__ void vm_wait()
 {
-  u32x4 q0, q1;
-  asm volatile("s_waitcnt vmcnt(%3)\n\t"
-               "ds_read_b128 %0, %2\n\t"
-               "ds_read_b128 %1, %2 offset:1024\n\t"
-               "s_waitcnt lgkmcnt(0)"
-               : "=&v"(q0), "=&v"(q1) : "v"(laddr), "i"(2 * (kBjRing - 2)) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory");
+}
+
+// This lane's 32 bytes of a ring slot (ordinary LDS loads: the compiler places the lgkmcnt wait at
+// the first use, one chain iteration later).
+__device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, uint32_t (&y)[8])
+{
+  const u32x4 q0 = *reinterpret_cast<const u32x4*>(slot + lane * 16u);
+  const u32x4 q1 = *reinterpret_cast<const u32x4*>(slot + 1024u + lane * 16u);
   y[0] = q0[0]; y[1] = q0[1]; y[2] = q0[2]; y[3] = q0[3];
   y[4] = q1[0]; y[5] = q1[1]; y[6] = q1[2]; y[7] = q1[3];
 }
@@ -456,7 +459,7 @@ __device__ __forceinline__ void ring_read(uint32_t laddr, uint32_t (&y)[kBjPlane
 template <int R, int RT, bool DEC, int ABL = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
-                                            uint32_t ring)
+                                            const uint8_t* ring_p, uint32_t ring)
 {
   const size_t stride = a.stride;
   const uint32_t k = a.k;
@@ -471,16 +474,18 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   constexpr int NJ = R == 16 ? 2 : 1;     // u32x16 offset vectors per source
   // Offsets and plan entries are loaded with ordinary uniform loads through the constant address
   // space (s_load, waits placed by the compiler).
-  // decode: plan_in entry i via the dword holding it (4-byte aligned scalar load, then shift)
+  // decode: plan_in entry i via the dword holding it (4-byte aligned scalar load); the shift that
+  // selects the entry is applied at the use, so the load's wait lands one iteration later.
   auto in_word = [&](uint32_t i) -> uint32_t {
     const uintptr_t ad = reinterpret_cast<uintptr_t>(in + i);
-    return const_load<uint32_t>(reinterpret_cast<const void*>(ad & ~static_cast<uintptr_t>(3))) >>
-           (8u * (ad & 2u));
+    return const_load<uint32_t>(reinterpret_cast<const void*>(ad & ~static_cast<uintptr_t>(3)));
+  };
+  auto in_shift = [&](uint32_t i) -> uint32_t {
+    return 8u * (static_cast<uint32_t>(reinterpret_cast<uintptr_t>(in + i)) & 2u);
   };
   auto row_of = [&](uint32_t i, uint32_t w) -> const uint8_t* {
     if constexpr (DEC) {
-      (void)i;
-      const uint32_t ii = w & 0xFFFFu;
+      const uint32_t ii = (w >> in_shift(i)) & 0xFFFFu;
       return ii < k ? base0 + ii * stride : base1 + (ii - k) * stride;
     } else {
       (void)w;
@@ -495,7 +500,9 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[j][p] = 0;
 
-  // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait count is constant).
+  // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait counts are constant);
+  // source 0 read into registers.  Steady state at iteration i: source i in registers, the LDS
+  // read of source i+1 in flight, DMAs of i+2 .. i+kBjRing-1 in flight.
 #pragma unroll
   for (int q = 0; q < kBjRing - 1; ++q) {
     const uint32_t iq = clampk(q);
@@ -507,14 +514,22 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   u32x16 on[NJ];
 #pragma unroll
   for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + 16 * h);
-  const uint32_t lane_off = lane * 16u;
+  uint32_t ycur[8];
+  vm_wait<2 * (kBjRing - 2)>();
+  ring_read(ring_p, lane, ycur);
   for (uint32_t i = 0; i < k; ++i) {
     u32x16 o[NJ];
 #pragma unroll
     for (int h = 0; h < NJ; ++h) o[h] = on[h];
     uint32_t Y[kBjPlanes];
-    ring_read(ring + (i % kBjRing) * kBjSlot + lane_off, Y);
-    {   // refill the slot read last iteration with source i + kBjRing - 1
+#pragma unroll
+    for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
+    if constexpr (!(ABL & 1)) transpose8(Y);   // consume ycur before its registers are reloaded
+    // source i+1: its DMA (issued kBjRing-2 iterations ago) has landed once only the DMAs of
+    // i+2 .. i+kBjRing-2 remain; start its LDS read now, consume it next iteration
+    vm_wait<2 * (kBjRing - 3)>();
+    ring_read(ring_p + ((i + 1) % kBjRing) * kBjSlot, lane, ycur);
+    {   // refill the slot of source i-1 (read and consumed) with source i + kBjRing - 1
       const uint32_t iq = clampk(i + kBjRing - 1);
       const uint8_t* row = row_of(iq, wn);
       dma_source(row + x0, row + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
@@ -523,7 +538,6 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     const uint32_t i1 = clampk(i + 1);
 #pragma unroll
     for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + static_cast<size_t>(i1) * jstep + 16 * h);
-    if constexpr (!(ABL & 1)) transpose8(Y);
     if constexpr (!(ABL & 2)) {
       NTC_BJ_XTIME(Y)
     } else {
@@ -597,15 +611,16 @@ __global__ __launch_bounds__(256) void gf_mac_bj(MacArgs a)
   const uint32_t row0 = tile * RT;
   if (row0 >= total) return;
   const uint32_t nrows = min(static_cast<uint32_t>(RT), total - row0);
-  const uint32_t ring = lds_addr(s_ring) + wave * (kBjRing * kBjSlot);
+  const uint8_t* ring_p = s_ring + wave * (kBjRing * kBjSlot);
+  const uint32_t ring = lds_addr(ring_p);
   if constexpr (RT == 16) {
     if (nrows > 8) {
-      mac_tile_bj<16, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring);
+      mac_tile_bj<16, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
       return;
     }
   }
-  if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring);
-  else mac_tile_bj<4, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring);
+  if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
+  else mac_tile_bj<4, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
 }
 
 // Encode (DEC = false): rep[g][rows] = C_g * src[g]; decode (DEC = true): the plan's D_g applied to

@@ -11,11 +11,12 @@ import collections
 import csv
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"encode_mac": ("gf_mac_bj<false>", "gf_mac<2, false>"),
-           "decode_mac": ("gf_mac_bj<true>", "gf_mac<2, true>")}
+KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
+           "decode_mac": (r"gf_mac_bj<\d+, true", r"gf_mac<\d, true")}
 
 
 def means(path, counter):
@@ -29,7 +30,7 @@ def means(path, counter):
 
 def pick(table, names):
     for k, v in table.items():
-        if any(n in k for n in names):
+        if any(re.search(n, k) for n in names):
             return v
     return None
 

@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libntc_gf256.so")
+# NTC_GF256_LIB points at an alternative build of the same library (A/B experiments only).
+LIB_PATH = os.environ.get("NTC_GF256_LIB") or os.path.join(HERE, "libntc_gf256.so")
 
 # Every symbol include/netcode/gpu.h declares (tests check the .so exports all of them).
 GPU_H_SYMBOLS = [

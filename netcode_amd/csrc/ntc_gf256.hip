@@ -356,11 +356,15 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
 // the byte-domain kernel.
 #include "gf_bitslice_chain.inc"
 
+// Delta swap of the `mask` bit groups of b with the groups `sh` bits higher in a: two shifts and
+// two bit-field inserts (v_bfi_b32 / v_bitop3), 4 VALU.
 __device__ __forceinline__ void swap_blocks(uint32_t& a, uint32_t& b, uint32_t sh, uint32_t mask)
 {
-  const uint32_t t = ((a >> sh) ^ b) & mask;
-  b ^= t;
-  a ^= t << sh;
+  // bitop3 0xCA = S0 ? S1 : S2 (bitwise select)
+  const uint32_t na = __builtin_amdgcn_bitop3_b32(mask << sh, b << sh, a, 0xCA);
+  const uint32_t nb = __builtin_amdgcn_bitop3_b32(mask, a >> sh, b, 0xCA);
+  a = na;
+  b = nb;
 }
 
 __device__ __forceinline__ void transpose8(uint32_t* d)
@@ -387,22 +391,29 @@ __device__ __forceinline__ T const_load(const void* p)
       reinterpret_cast<uintptr_t>(p));
 }
 
-// Block offsets of one (generation, source, row tile): 2*RT sites = RT rows x 2 nibbles.
+// Block offsets of one (generation, source, row tile): 2*RT sites = RT rows x 2 nibbles.  A thread
+// writes 4 consecutive sites (2 rows) as one 16-byte store.
 __global__ __launch_bounds__(256) void bj_offsets(const uint8_t* __restrict__ coef, uint32_t rp,
-                                                  uint32_t rt, uint32_t ntiles, uint64_t total,
+                                                  uint32_t rt, uint32_t ntiles, uint64_t total4,
                                                   uint32_t* __restrict__ joff)
 {
   const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  if (idx >= total) return;
-  const uint32_t nsites = 2u * rt;
-  const uint32_t site = static_cast<uint32_t>(idx % nsites);
-  const uint64_t q = idx / nsites;
+  if (idx >= total4) return;
+  const uint32_t quads = rt / 2u;                     // 4-site groups per tile
+  const uint32_t qd = static_cast<uint32_t>(idx % quads);
+  const uint64_t q = idx / quads;
   const uint32_t tile = static_cast<uint32_t>(q % ntiles);
   const uint64_t gk = q / ntiles;
-  const uint32_t j = tile * rt + (site >> 1);
-  const uint32_t c = j < rp ? coef[gk * rp + j] : 0u;
-  const uint32_t v = (c >> (4u * (site & 1u))) & 15u;
-  joff[idx] = site * kBjSite + kBjVo[v];
+  const uint32_t j0 = tile * rt + 2u * qd;
+  const uint32_t c0 = j0 < rp ? coef[gk * rp + j0] : 0u;
+  const uint32_t c1 = j0 + 1 < rp ? coef[gk * rp + j0 + 1] : 0u;
+  const uint32_t s0 = 4u * qd * kBjSite;
+  uint4 o;
+  o.x = s0 + kBjVo[c0 & 15u];
+  o.y = s0 + kBjSite + kBjVo[c0 >> 4];
+  o.z = s0 + 2u * kBjSite + kBjVo[c1 & 15u];
+  o.w = s0 + 3u * kBjSite + kBjVo[c1 >> 4];
+  reinterpret_cast<uint4*>(joff)[idx] = o;
 }
 
 // Source staging: every wave streams its sources through a private ring of kBjRing LDS slots with
@@ -1135,8 +1146,9 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
     if (rc) return rc;
     a.joff = static_cast<const uint32_t*>(e->joff);
-    hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
-                       a.coef, a.rp, rt, a.ntiles, n, static_cast<uint32_t*>(e->joff));
+    const uint64_t n4 = n / 4;
+    hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n4 + 255) / 256)), dim3(256), 0, st,
+                       a.coef, a.rp, rt, a.ntiles, n4, static_cast<uint32_t*>(e->joff));
     if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
   } else {
     const int D = pick_d(a.stride);

@@ -23,7 +23,8 @@ Usage: python tools/gen_bitslice_chain.py   (rewrites the .inc; commit the resul
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-OUT = os.path.join(os.path.dirname(HERE), "netcode_amd", "csrc", "gf_bitslice_chain.inc")
+OUT = os.environ.get("NTC_BJ_OUT") or os.path.join(os.path.dirname(HERE), "netcode_amd", "csrc",
+                                                 "gf_bitslice_chain.inc")
 TILES = (16, 8, 4)
 
 
@@ -35,8 +36,9 @@ def valu_bytes(v):
     return {0: 0, 1: 32, 2: 64, 3: 96, 4: 128}[popcount(v)]
 
 
-TAIL = 16      # s_add [+ s_addc] + s_setpc, padded so every block starts 16-byte aligned
-SIZES = [valu_bytes(v) + TAIL for v in range(16)]
+TAIL = 12      # s_add [+ s_addc] + s_setpc
+ALIGN = int(os.environ.get("NTC_BJ_ALIGN", "16"))   # every block starts ALIGN-byte aligned
+SIZES = [(valu_bytes(v) + TAIL + ALIGN - 1) // ALIGN * ALIGN for v in range(16)]
 VO = [sum(SIZES[:v]) for v in range(16)]
 SITE = sum(SIZES)
 

@@ -115,8 +115,8 @@ def chain_lines(y, R):
              "s_add_u32 s98, s96, %[o0]",
              "s_setpc_b64 s[98:99]", ".p2align 6", "Ltf%=:"]
     lines += tables(y, R, safe=False)
-    lines += ["Lsafe%=:", "s_getpc_b64 s[96:97]", "Lg2%=:",
-              "s_add_u32 s96, s96, Lts%= - Lg2%=", "s_addc_u32 s97, s97, 0",
+    lines += ["Lsafe%=:", "s_getpc_b64 s[96:97]", "Lh%=:",
+              "s_add_u32 s96, s96, Lts%= - Lh%=", "s_addc_u32 s97, s97, 0",
               "s_add_u32 s98, s96, %[o0]", "s_addc_u32 s99, s97, 0",
               "s_setpc_b64 s[98:99]", ".p2align 6", "Lts%=:"]
     lines += tables(y, R, safe=True)

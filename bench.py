@@ -267,11 +267,19 @@ def main():
             traffic = tj.get(a.config, {}).get(dom)
         except Exception:
             traffic = None
+    valu = None
+    vfile = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if os.path.exists(vfile):
+        try:
+            valu = json.load(open(vfile)).get(a.config, {}).get(dom)
+        except Exception:
+            valu = None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": dom,
             "kernel_ms": round(t_dom, 4), "algorithmic_bytes_per_launch": int(bytes_dom),
             "byte_macs_per_launch": int(macs),
-            "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2)}
+            "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2),
+            "valu_profile": valu}
 
     line = {"metric": "device-resident GF(256) encode+decode GiB/s, k=128 r=32, 4 KiB pkts, 1/2/4/8 GPU",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,

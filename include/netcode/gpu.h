@@ -115,6 +115,27 @@ int  ntc_gf256_combine_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint
                              uint32_t stride, const uint8_t* in, const uint8_t* coef,
                              uint8_t* out, void* stream);
 
+/* ---- Dense codes: caller-supplied coefficient matrices (BASELINE config 5 extension) --------
+ * The reference's w = 8 schedule cannot build large invertible systems (coefficient() has period
+ * 255), so k = 1024 "all sources lost" decoding uses a dense matrix chosen by the caller.
+ * mat [G][n][n] row-major, row j = coefficients of repair j over sources 0..n-1 (rep = mat * src).
+ *
+ * ntc_gf256_dense_invert_batch  <- ntc::detail::invert (invert_matrix.cc:9-128) for n <= 1024:
+ *   inv [G][n][n] = mat^-1 (the inverse is unique; device blocked Gauss-Jordan).  ok[g] = 1 if
+ *   mat[g] is invertible, 0 if singular (inv[g] is then all zero).  ok may be NULL.
+ * ntc_gf256_dense_encode_batch  <- detail::encoder (encoder.cc:15-64) with mat [G][r][k] in place
+ *   of the coefficient schedule: rep[g][j] = sum_i mat[g][j][i] * src[g][i] over `stride` bytes.
+ * ntc_gf256_dense_decode_batch  <- attempt_full_decoding's invert + MAC (decoder.cc:412-534):
+ *   out[g] = mat[g]^-1 * rep[g] ([G][n][stride]); ok[g] as above (out[g] zero when singular). */
+int  ntc_gf256_dense_invert_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t n,
+                                  const uint8_t* mat, uint8_t* inv, uint8_t* ok, void* stream);
+int  ntc_gf256_dense_encode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
+                                  uint32_t stride, const uint8_t* mat, const uint8_t* src,
+                                  uint8_t* rep, void* stream);
+int  ntc_gf256_dense_decode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t n, uint32_t stride,
+                                  const uint8_t* mat, const uint8_t* rep, uint8_t* out,
+                                  uint8_t* ok, void* stream);
+
 /* dst = c*src (add = 0) or dst ^= c*src (add = 1) over `len` bytes of device memory. */
 int  ntc_gf256_region_multiply(ntc_gf256_engine* eng, const uint8_t* src, uint8_t* dst,
                                size_t len, uint8_t c, int add, void* stream);

@@ -20,6 +20,7 @@ GPU_H_SYMBOLS = [
     "ntc_gf256_combine_batch", "ntc_gf256_coefficient",
     "ntc_gf256_multiply_size", "ntc_gf256_multiply", "ntc_gf256_invert",
     "ntc_gf256_last_error", "ntc_gf256_build_info",
+    "ntc_gf256_dense_invert_batch", "ntc_gf256_dense_encode_batch", "ntc_gf256_dense_decode_batch",
 ]
 
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "EUNSUPPORTED"}
@@ -66,6 +67,9 @@ def load(path: str | None = None):
     L.ntc_gf256_coef_pitch.argtypes = [u32]
     L.ntc_gf256_coef_pitch.restype = u32
     L.ntc_gf256_combine_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, V]
+    L.ntc_gf256_dense_invert_batch.argtypes = [V, u32, u32, P, P, P, V]
+    L.ntc_gf256_dense_encode_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, V]
+    L.ntc_gf256_dense_decode_batch.argtypes = [V, u32, u32, u32, P, P, P, P, V]
     L.ntc_gf256_coefficient.argtypes = [u32, u32]
     L.ntc_gf256_coefficient.restype = u32
     L.ntc_gf256_multiply_size.argtypes = [u16, u32]

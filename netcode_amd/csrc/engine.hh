@@ -1,0 +1,49 @@
+// engine.hh -- engine state and helpers shared by the engine's translation units
+// (ntc_gf256.hip: reference-schedule encode/decode + MAC kernels; ntc_dense.hip: dense codes).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "netcode/gpu.h"
+
+struct ntc_gf256_engine {
+  int device = 0;
+  size_t plan_cap_G = 0, plan_cap_k = 0, plan_cap_rp = 0;
+  uint16_t* plan_m = nullptr;
+  uint16_t* plan_in = nullptr;
+  uint16_t* plan_out = nullptr;
+  uint8_t* plan_coef = nullptr;
+  void* enc_coef = nullptr;
+  size_t enc_coef_cap = 0;
+  void* joff = nullptr;        // bit-sliced MAC block offsets
+  size_t joff_cap = 0;
+  int mac_kind = NTC_GF256_MAC_AUTO;
+  // geometry of the last plan (decode_apply must match)
+  uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
+  // dense-code workspace (ntc_dense.hip): augmented matrices (ping-pong), panel trackers,
+  // pivot rows, row flags, combine coefficients
+  void* dn_x = nullptr;   size_t dn_x_cap = 0;
+  void* dn_y = nullptr;   size_t dn_y_cap = 0;
+  void* dn_w = nullptr;   size_t dn_w_cap = 0;
+  void* dn_piv = nullptr; size_t dn_piv_cap = 0;
+  void* dn_flag = nullptr; size_t dn_flag_cap = 0;
+  void* dn_coef = nullptr; size_t dn_coef_cap = 0;
+  void* dn_ok = nullptr;  size_t dn_ok_cap = 0;
+};
+
+namespace ntcgpu {
+
+// Record `msg` as this thread's last error (ntc_gf256_last_error) and return `code`.
+int fail(int code, const std::string& msg);
+// NTC_GPU_OK, or the mapped status with the HIP error text recorded.
+int hip_check(hipError_t e, const char* what);
+// Grow a device buffer to at least `need` bytes (contents not preserved).
+int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
+// Coefficient rows padded to the MAC kernels' row tile (ntc_gf256_coef_pitch).
+uint32_t tile_rp(uint32_t r);
+
+}  // namespace ntcgpu

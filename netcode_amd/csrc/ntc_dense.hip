@@ -1,0 +1,427 @@
+// ntc_dense.hip -- dense GF(2^8) codes on MI355X (gfx950): batched device Gauss-Jordan + combine.
+//
+// BASELINE config 5 / SURVEY §8(f)3: k = 1024 sources, every one lost, k repairs each covering all
+// k with a *non-reference* dense coefficient matrix (the reference's w = 8 schedule makes every such
+// matrix singular: coefficient() has period 255, galois_field.hh:143-158).  Decoding is then
+// "invert M, apply M^-1": the work of detail::invert (invert_matrix.cc:9-128) followed by the
+// region MAC loop of attempt_full_decoding (detail/decoder.cc:503-534), at sizes the reference's
+// m x m scalar path was never meant for.
+//
+// Inversion: blocked Gauss-Jordan on the augmented matrix X = [A | I] (np x 2np bytes per
+// generation, np = n rounded up to the 32-column panel; A is embedded in the identity so padding
+// never changes invertibility or the top-left block of the inverse).  Per panel of 32 columns:
+//   dn_panel   one workgroup per generation, one thread per row (np <= 1024 threads): 32 pivot
+//              steps over a 9-dword live window of the row (the panel columns still to eliminate
+//              + the tracker columns already assigned), one barrier per step.  The tracker W
+//              records the panel's row operations: afterwards
+//                  row_i' = keep_i * row_i  XOR  sum_t W[t][i] * row_{piv_t}
+//              with keep_i = 0 for the 32 rows chosen as pivots in this panel.
+//   dn_update  applies that to the columns right of the panel (and the identity half) as a
+//              GF(2^8) multiply-accumulate, X -> Y (ping-pong: pivot rows are read by every row).
+// Pivoting takes the lowest-index eligible row with a non-zero entry; the inverse is unique, so
+// the result is the reference's M^-1 whatever the pivot order, and singularity is a rank property.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "engine.hh"
+#include "gf256_field.hh"
+#include "netcode/gpu.h"
+
+namespace ntcgpu {
+namespace dense {
+
+__constant__ __attribute__((aligned(16))) PermTables dn_perm = make_perm_tables();
+__constant__ __attribute__((aligned(16))) FieldTables dn_field = make_field_tables();
+
+constexpr uint32_t kPanel = 32;       // pivot columns per panel
+constexpr uint32_t kMaxN = 1024;      // one thread per row in dn_panel
+constexpr int kUpdRows = 8;           // rows per wave in dn_update
+constexpr uint32_t kUpdSpan = 512;    // columns per wave in dn_update (64 lanes x 8 bytes)
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// c*x for the four bytes of x; t = the 5 table dwords of c (PermTables layout, 3/3/2-bit split).
+__device__ __forceinline__ uint32_t mul4(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                         uint32_t t4, uint32_t x)
+{
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t1, t0, x & 0x07070707u),
+                                     __builtin_amdgcn_perm(t3, t2, (x >> 3) & 0x07070707u),
+                                     __builtin_amdgcn_perm(t4, t4, (x >> 6) & 0x03030303u), 0x96);
+}
+
+template <typename T>
+__device__ __forceinline__ T const_load(const void* p)
+{
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
+// X[g] = [A | I]: A = mat[g] (n x n) inside an np x np identity.  Row flags: eligible = 1.
+__global__ __launch_bounds__(256) void dn_init(const uint8_t* __restrict__ mat, uint32_t n,
+                                               uint32_t np, uint8_t* __restrict__ X,
+                                               uint8_t* __restrict__ flag, uint8_t* __restrict__ ok)
+{
+  const uint32_t i = blockIdx.x, g = blockIdx.y, P = 2 * np;
+  uint8_t* row = X + (static_cast<size_t>(g) * np + i) * P;
+  const uint8_t* mrow = mat + (static_cast<size_t>(g) * n + i) * n;
+  for (uint32_t c = threadIdx.x; c < P; c += blockDim.x) {
+    uint8_t v;
+    if (c < np) v = (i < n && c < n) ? mrow[c] : static_cast<uint8_t>(i == c);
+    else v = static_cast<uint8_t>(c - np == i);
+    row[c] = v;
+  }
+  if (threadIdx.x == 0) {
+    flag[static_cast<size_t>(g) * np + i] = 1;
+    if (i == 0) ok[g] = 1;
+  }
+}
+
+struct PanelArgs {
+  uint32_t np, c0;
+  const uint8_t* X;
+  uint8_t* W;          // [G][32][np] tracker, t-major
+  uint32_t* piv;       // [G][np] pivot row of column c
+  uint8_t* flag;       // [G][np] 1 = not yet a pivot row (eligible)
+  uint8_t* keep;       // [G][np] 0 = chosen as a pivot in this panel
+  uint8_t* ok;         // [G] 0 once singular
+};
+
+// One workgroup per generation, thread i = row i.  v[0..7]: the row's 32 panel bytes; v[8..15]:
+// its 32 tracker bytes.  At step t only dwords [t/4, 8) of the panel and [8, 8 + t/4] of the
+// tracker can be non-zero in a candidate row (earlier pivot columns are eliminated, later tracker
+// columns not yet assigned), so every step moves and multiplies exactly 9 dwords.
+__global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
+{
+  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
+  __shared__ uint8_t exp_t[512];
+  __shared__ uint8_t log_t[256];
+  __shared__ uint32_t cmask[3];
+  __shared__ uint32_t crow[2][16];
+  __shared__ __attribute__((aligned(16))) uint32_t cbuf[2][16][16];
+
+  const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
+  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+  for (uint32_t e = i; e < 512; e += blockDim.x) exp_t[e] = dn_field.exp[e];
+  for (uint32_t e = i; e < 256; e += blockDim.x) log_t[e] = dn_field.log[e];
+  if (i < 3) cmask[i] = 0;
+  const bool live = a.ok[g] != 0;
+  __syncthreads();
+  if (!live) return;                                   // uniform: a singular generation stops
+
+  const uint32_t np = a.np, P = 2 * np;
+  const bool row_ok = i < np;
+  const size_t gi = static_cast<size_t>(g) * np + i;
+  uint32_t v[16];
+  if (row_ok) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
+    const u32x4 q0 = src[0], q1 = src[1];
+    v[0] = q0[0]; v[1] = q0[1]; v[2] = q0[2]; v[3] = q0[3];
+    v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
+  } else {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) v[d] = 0;
+  }
+#pragma unroll
+  for (int d = 8; d < 16; ++d) v[d] = 0;
+  bool elig = row_ok && a.flag[gi] != 0;
+  bool chosen = false;
+  bool singular = false;
+
+#pragma unroll
+  for (int t = 0; t < static_cast<int>(kPanel); ++t) {
+    const int q = t >> 2, sh = 8 * (t & 3), par = t & 1;
+    const uint32_t f = (v[q] >> sh) & 0xFFu;
+    const uint64_t b = __ballot(elig && f != 0);
+    if (b != 0 && lane == static_cast<uint32_t>(__ffsll(static_cast<long long>(b)) - 1)) {
+      // this wave's candidate: publish its live window with tracker column t set (the row in the
+      // pivot basis: it stops counting as itself and becomes pivot t)
+#pragma unroll
+      for (int d = q; d < 8; ++d) cbuf[par][w][d] = v[d];
+#pragma unroll
+      for (int d = 8; d <= 8 + q; ++d) cbuf[par][w][d] = v[d] ^ (d == 8 + q ? (1u << sh) : 0u);
+      crow[par][w] = i;
+      atomicOr(&cmask[t % 3], 1u << w);
+    }
+    __syncthreads();
+    const uint32_t m = cmask[t % 3];
+    if (i == 0) cmask[(t + 2) % 3] = 0;                // next used at step t + 2
+    if (m == 0) { singular = true; break; }            // uniform
+    const uint32_t ws = __ffs(m) - 1;                  // lowest wave = lowest row index
+    const uint32_t prow = crow[par][ws];
+    const uint32_t pv = (cbuf[par][ws][q] >> sh) & 0xFFu;
+    const uint32_t lpv = log_t[pv];
+    uint32_t c = 0;
+    if (i == prow) {
+      c = exp_t[255 - lpv];                            // 1 / pivot (pv != 0)
+      chosen = true;
+      elig = false;
+#pragma unroll
+      for (int d = q; d < 8; ++d) v[d] = 0;
+#pragma unroll
+      for (int d = 8; d <= 8 + q; ++d) v[d] = 0;
+    } else if (f != 0) {
+      c = exp_t[log_t[f] + 255 - lpv];                 // f / pivot
+    }
+    if (i == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + t] = prow;
+    if (c != 0) {
+      const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
+      const uint32_t t4 = perm_t[c][4];
+#pragma unroll
+      for (int d = q; d < 8; ++d) v[d] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, cbuf[par][ws][d]);
+#pragma unroll
+      for (int d = 8; d <= 8 + q; ++d) v[d] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, cbuf[par][ws][d]);
+    }
+  }
+  if (singular) {
+    if (i == 0) a.ok[g] = 0;
+    return;
+  }
+  if (row_ok) {
+    a.flag[gi] = elig ? 1 : 0;
+    a.keep[gi] = chosen ? 0 : 1;
+    uint8_t* wg = a.W + static_cast<size_t>(g) * kPanel * np + i;
+#pragma unroll
+    for (int t = 0; t < static_cast<int>(kPanel); ++t)
+      wg[static_cast<size_t>(t) * np] = static_cast<uint8_t>(v[8 + (t >> 2)] >> (8 * (t & 3)));
+  }
+}
+
+struct UpdArgs {
+  uint32_t G, np, c0, cs;      // cs: first column to produce
+  uint32_t ntiles, nspans;
+  const uint8_t* X;
+  uint8_t* Y;
+  const uint8_t* W;
+  const uint32_t* piv;
+  const uint8_t* keep;
+  const uint8_t* ok;
+};
+
+// One wave per (generation, 8-row tile, 512-column span of [cs, 2np)):
+//   Y[i][c] = keep_i * X[i][c]  XOR  sum_t W[t][i] * X[piv_t][c]
+__global__ __launch_bounds__(256) void dn_update(UpdArgs a)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t span = task % a.nspans;
+  task /= a.nspans;
+  const uint32_t tile = task % a.ntiles;
+  const uint32_t g = task / a.ntiles;
+  if (g >= a.G) return;
+  if (__builtin_amdgcn_readfirstlane(a.ok[g]) == 0) return;
+  const uint32_t np = a.np, P = 2 * np;
+  const uint32_t col = a.cs + span * kUpdSpan + lane * 8u;
+  const bool active = col < P;
+  const uint32_t cx = active ? col : a.cs;
+  const uint8_t* Xg = a.X + static_cast<size_t>(g) * np * P;
+  uint8_t* Yg = a.Y + static_cast<size_t>(g) * np * P;
+  const uint32_t i0 = tile * kUpdRows;
+  const uint8_t* keep = a.keep + static_cast<size_t>(g) * np + i0;
+  const uint32_t* piv = a.piv + static_cast<size_t>(g) * np + a.c0;
+  const uint8_t* Wg = a.W + static_cast<size_t>(g) * kPanel * np + i0;
+
+  uint32_t acc[kUpdRows][2];
+  const u32x2 kw = const_load<u32x2>(keep);
+#pragma unroll
+  for (int j = 0; j < kUpdRows; ++j) {
+    const uint32_t kj = (kw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    if (kj) {
+      const u32x2 x = *reinterpret_cast<const u32x2*>(Xg + static_cast<size_t>(i0 + j) * P + cx);
+      acc[j][0] = x[0];
+      acc[j][1] = x[1];
+    } else {
+      acc[j][0] = acc[j][1] = 0;
+    }
+  }
+#pragma unroll 4
+  for (uint32_t t = 0; t < kPanel; ++t) {
+    const uint32_t prow = const_load<uint32_t>(piv + t);
+    const u32x2 x = *reinterpret_cast<const u32x2*>(Xg + static_cast<size_t>(prow) * P + cx);
+    const u32x2 cw = const_load<u32x2>(Wg + static_cast<size_t>(t) * np);
+#pragma unroll
+    for (int j = 0; j < kUpdRows; ++j) {
+      const uint32_t c = (cw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      if (c) {
+        const u32x4 tab = const_load<u32x4>(&dn_perm.w[c][0]);
+        const uint32_t t4 = const_load<uint32_t>(&dn_perm.w[c][4]);
+        acc[j][0] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, x[0]);
+        acc[j][1] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, x[1]);
+      }
+    }
+  }
+  if (!active) return;
+#pragma unroll
+  for (int j = 0; j < kUpdRows; ++j) {
+    u32x2 o;
+    o[0] = acc[j][0];
+    o[1] = acc[j][1];
+    *reinterpret_cast<u32x2*>(Yg + static_cast<size_t>(i0 + j) * P + col) = o;
+  }
+}
+
+// inv[g][t][0..n) = X[g][piv[t]][np .. np + n)  (zeros for a singular generation)
+__global__ __launch_bounds__(256) void dn_gather_inv(uint32_t n, uint32_t np, const uint8_t* __restrict__ X,
+                                                     const uint32_t* __restrict__ piv,
+                                                     const uint8_t* __restrict__ ok, uint8_t* __restrict__ inv)
+{
+  const uint32_t t = blockIdx.x, g = blockIdx.y, P = 2 * np;
+  const bool good = ok[g] != 0;
+  const uint8_t* src = X + (static_cast<size_t>(g) * np + (good ? piv[static_cast<size_t>(g) * np + t] : 0)) * P + np;
+  uint8_t* dst = inv + (static_cast<size_t>(g) * n + t) * n;
+  for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) dst[c] = good ? src[c] : 0;
+}
+
+// dst[g][c][r] = src[g][r][c] (src [G][R][C], dst [G][C][pitch], pitch >= R; entries r >= R of a
+// dst row are zeroed).  64 x 64 tiles through LDS.
+__global__ __launch_bounds__(256) void dn_transpose(uint32_t R, uint32_t C, uint32_t pitch,
+                                                    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst)
+{
+  __shared__ uint8_t tile[64][65];
+  const uint32_t g = blockIdx.z;
+  const uint32_t r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const uint32_t tx = threadIdx.x & 63u, ty = threadIdx.x >> 6;
+  const uint8_t* s = src + static_cast<size_t>(g) * R * C;
+  for (uint32_t y = ty; y < 64; y += 4) {
+    const uint32_t r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < R && c < C) ? s[static_cast<size_t>(r) * C + c] : 0;
+  }
+  __syncthreads();
+  uint8_t* d = dst + static_cast<size_t>(g) * C * pitch;
+  for (uint32_t y = ty; y < 64; y += 4) {
+    const uint32_t c = c0 + y, r = r0 + tx;
+    if (c < C && r < pitch) d[static_cast<size_t>(c) * pitch + r] = tile[tx][y];
+  }
+}
+
+}  // namespace dense
+}  // namespace ntcgpu
+
+using namespace ntcgpu;
+using namespace ntcgpu::dense;
+
+namespace {
+
+// Blocked Gauss-Jordan of G n x n matrices; on return (stream order) the inverse rows sit in the
+// engine's X buffer (rows permuted by piv) and ok[g] says whether generation g was invertible.
+int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat, hipStream_t st,
+                 const uint8_t** Xout, uint32_t* np_out)
+{
+  const uint32_t np = (n + kPanel - 1) / kPanel * kPanel;
+  const size_t xb = static_cast<size_t>(G) * np * 2 * np;
+  int rc;
+  if ((rc = ensure_buf(&e->dn_x, &e->dn_x_cap, xb, "hipMalloc dense X"))) return rc;
+  if ((rc = ensure_buf(&e->dn_y, &e->dn_y_cap, xb, "hipMalloc dense Y"))) return rc;
+  if ((rc = ensure_buf(&e->dn_w, &e->dn_w_cap, static_cast<size_t>(G) * kPanel * np + 16, "hipMalloc dense W"))) return rc;
+  if ((rc = ensure_buf(&e->dn_piv, &e->dn_piv_cap, static_cast<size_t>(G) * np * 4 + 16, "hipMalloc dense piv"))) return rc;
+  if ((rc = ensure_buf(&e->dn_flag, &e->dn_flag_cap, static_cast<size_t>(G) * np * 2 + 16, "hipMalloc dense flags"))) return rc;
+  if ((rc = ensure_buf(&e->dn_ok, &e->dn_ok_cap, G + 16, "hipMalloc dense ok"))) return rc;
+  uint8_t* X = static_cast<uint8_t*>(e->dn_x);
+  uint8_t* Y = static_cast<uint8_t*>(e->dn_y);
+  uint8_t* flag = static_cast<uint8_t*>(e->dn_flag);
+  uint8_t* keep = flag + static_cast<size_t>(G) * np;
+  uint8_t* ok = static_cast<uint8_t*>(e->dn_ok);
+  hipLaunchKernelGGL(dn_init, dim3(np, G), dim3(256), 0, st, mat, n, np, X, flag, ok);
+  if ((rc = hip_check(hipGetLastError(), "dn_init launch"))) return rc;
+  const uint32_t threads = (np + 63) / 64 * 64;
+  for (uint32_t c0 = 0; c0 < np; c0 += kPanel) {
+    PanelArgs pa{np, c0, X, static_cast<uint8_t*>(e->dn_w), static_cast<uint32_t*>(e->dn_piv), flag, keep, ok};
+    hipLaunchKernelGGL(dn_panel, dim3(G), dim3(threads), 0, st, pa);
+    if ((rc = hip_check(hipGetLastError(), "dn_panel launch"))) return rc;
+    UpdArgs ua{};
+    ua.G = G; ua.np = np; ua.c0 = c0;
+    // the A half left of the next panel is never read again; the last panel only needs the I half
+    ua.cs = c0 + kPanel < np ? c0 + kPanel : np;
+    ua.ntiles = np / kUpdRows;
+    ua.nspans = (2 * np - ua.cs + kUpdSpan - 1) / kUpdSpan;
+    ua.X = X; ua.Y = Y; ua.W = static_cast<const uint8_t*>(e->dn_w);
+    ua.piv = static_cast<const uint32_t*>(e->dn_piv); ua.keep = keep; ua.ok = ok;
+    const uint64_t waves = static_cast<uint64_t>(G) * ua.ntiles * ua.nspans;
+    hipLaunchKernelGGL(dn_update, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(256), 0, st, ua);
+    if ((rc = hip_check(hipGetLastError(), "dn_update launch"))) return rc;
+    uint8_t* tmp = X; X = Y; Y = tmp;
+  }
+  *Xout = X;
+  *np_out = np;
+  return NTC_GPU_OK;
+}
+
+int copy_ok(ntc_gf256_engine* e, uint32_t G, uint8_t* ok, hipStream_t st)
+{
+  if (!ok) return NTC_GPU_OK;
+  return hip_check(hipMemcpyAsync(ok, e->dn_ok, G, hipMemcpyDeviceToDevice, st), "copy ok flags");
+}
+
+}  // namespace
+
+extern "C" {
+
+int ntc_gf256_dense_invert_batch(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat,
+                                 uint8_t* inv, uint8_t* ok, void* stream)
+{
+  if (!e || !mat || !inv) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (G == 0 || n == 0) return fail(NTC_GPU_EINVAL, "G and n must be > 0");
+  if (n > kMaxN) return fail(NTC_GPU_EUNSUPPORTED, "dense inversion supports n <= 1024");
+  if (G > 65535) return fail(NTC_GPU_EUNSUPPORTED, "G > 65535");
+  (void)hipSetDevice(e->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint8_t* X;
+  uint32_t np;
+  int rc = dense_invert(e, G, n, mat, st, &X, &np);
+  if (rc) return rc;
+  hipLaunchKernelGGL(dn_gather_inv, dim3(n, G), dim3(256), 0, st, n, np, X,
+                     static_cast<const uint32_t*>(e->dn_piv), static_cast<const uint8_t*>(e->dn_ok), inv);
+  if ((rc = hip_check(hipGetLastError(), "dn_gather_inv launch"))) return rc;
+  return copy_ok(e, G, ok, st);
+}
+
+int ntc_gf256_dense_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
+                                 uint32_t stride, const uint8_t* mat, const uint8_t* src,
+                                 uint8_t* rep, void* stream)
+{
+  if (!e || !mat || !src || !rep) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (G == 0 || k == 0 || r == 0) return fail(NTC_GPU_EINVAL, "G, k and r must be > 0");
+  if (G > 65535) return fail(NTC_GPU_EUNSUPPORTED, "G > 65535");
+  (void)hipSetDevice(e->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint32_t pitch = ntc_gf256_coef_pitch(r);
+  int rc = ensure_buf(&e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * k * pitch + 64, "hipMalloc dense coef");
+  if (rc) return rc;
+  // combine wants coef[g][i][j] (input-major): the transpose of mat[g][j][i]
+  hipLaunchKernelGGL(dn_transpose, dim3((k + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, r, k,
+                     pitch, mat, static_cast<uint8_t*>(e->dn_coef));
+  if ((rc = hip_check(hipGetLastError(), "dn_transpose launch"))) return rc;
+  return ntc_gf256_combine_batch(e, G, k, r, stride, src, static_cast<const uint8_t*>(e->dn_coef), rep, stream);
+}
+
+int ntc_gf256_dense_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t n, uint32_t stride,
+                                 const uint8_t* mat, const uint8_t* rep, uint8_t* out, uint8_t* ok,
+                                 void* stream)
+{
+  if (!e || !mat || !rep || !out) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (G == 0 || n == 0) return fail(NTC_GPU_EINVAL, "G and n must be > 0");
+  if (n > kMaxN) return fail(NTC_GPU_EUNSUPPORTED, "dense decoding supports n <= 1024");
+  if (G > 65535) return fail(NTC_GPU_EUNSUPPORTED, "G > 65535");
+  if (stride == 0 || stride % 16 != 0) return fail(NTC_GPU_EINVAL, "stride must be a positive multiple of 16");
+  (void)hipSetDevice(e->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint8_t* X;
+  uint32_t np;
+  int rc = dense_invert(e, G, n, mat, st, &X, &np);
+  if (rc) return rc;
+  // M^-1 rows into the Y buffer (free after the last swap), then transposed into combine layout:
+  // out[g][t] = sum_i inv[t][i] * rep[g][i]  ->  coef[g][i][t] = inv[t][i]
+  uint8_t* invbuf = static_cast<uint8_t*>(X == e->dn_x ? e->dn_y : e->dn_x);
+  hipLaunchKernelGGL(dn_gather_inv, dim3(n, G), dim3(256), 0, st, n, np, X,
+                     static_cast<const uint32_t*>(e->dn_piv), static_cast<const uint8_t*>(e->dn_ok), invbuf);
+  if ((rc = hip_check(hipGetLastError(), "dn_gather_inv launch"))) return rc;
+  const uint32_t pitch = ntc_gf256_coef_pitch(n);
+  if ((rc = ensure_buf(&e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * n * pitch + 64, "hipMalloc dense coef"))) return rc;
+  hipLaunchKernelGGL(dn_transpose, dim3((n + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, n, n,
+                     pitch, invbuf, static_cast<uint8_t*>(e->dn_coef));
+  if ((rc = hip_check(hipGetLastError(), "dn_transpose launch"))) return rc;
+  if ((rc = ntc_gf256_combine_batch(e, G, n, n, stride, rep, static_cast<const uint8_t*>(e->dn_coef), out, stream))) return rc;
+  return copy_ok(e, G, ok, st);
+}
+
+}  // extern "C"

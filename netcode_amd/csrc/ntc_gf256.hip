@@ -26,6 +26,7 @@
 #include <string>
 
 #include "gf256_field.hh"
+#include "engine.hh"
 #include "netcode/gpu.h"
 
 namespace ntcgpu {
@@ -1046,23 +1047,7 @@ __global__ __launch_bounds__(256) void region_mul(const uint8_t* __restrict__ sr
 // =================================================================================== C ABI ====
 using namespace ntcgpu;
 
-struct ntc_gf256_engine {
-  int device = 0;
-  size_t plan_cap_G = 0, plan_cap_k = 0, plan_cap_rp = 0;
-  uint16_t* plan_m = nullptr;
-  uint16_t* plan_in = nullptr;
-  uint16_t* plan_out = nullptr;
-  uint8_t* plan_coef = nullptr;
-  void* enc_coef = nullptr;
-  size_t enc_coef_cap = 0;
-  void* joff = nullptr;        // bit-sliced MAC block offsets
-  size_t joff_cap = 0;
-  int mac_kind = NTC_GF256_MAC_AUTO;
-  // geometry of the last plan (decode_apply must match)
-  uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
-};
-
-namespace {
+namespace ntcgpu {
 
 thread_local std::string g_err;
 
@@ -1078,6 +1063,10 @@ int hip_check(hipError_t e, const char* what)
   return fail(e == hipErrorOutOfMemory ? NTC_GPU_ENOMEM : NTC_GPU_EDEVICE,
               std::string(what) + ": " + hipGetErrorString(e));
 }
+
+}  // namespace ntcgpu
+
+namespace {
 
 uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
@@ -1122,8 +1111,6 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
   const uint32_t pieces = stride / 16, spans = (stride + 2047) / 2048;   // 16-B pieces per span: 128
   return pieces * 100 >= spans * 128 * 70;
 }
-
-int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
 
 // Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
 int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what)
@@ -1180,6 +1167,10 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   return hip_check(hipGetLastError(), what);
 }
 
+}  // namespace
+
+namespace ntcgpu {
+
 // Coefficient rows padded to the row tile the MAC kernel reads (4, 8, 16 or a multiple of 32).
 uint32_t tile_rp(uint32_t r)
 {
@@ -1200,6 +1191,10 @@ int ensure_buf(void** p, size_t* cap, size_t need, const char* what)
   *cap = need;
   return NTC_GPU_OK;
 }
+
+}  // namespace ntcgpu
+
+namespace {
 
 int ensure_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t rp)
 {
@@ -1287,6 +1282,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_coef);
   (void)hipFree(e->enc_coef);
   (void)hipFree(e->joff);
+  for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   delete e;
 }
 

@@ -237,3 +237,63 @@ class BatchDecoder:
 def status_to_numpy(status: torch.Tensor) -> np.ndarray:
     """[G, 12] uint8 device tensor -> structured numpy array (STATUS_DTYPE)."""
     return status.cpu().numpy().view(STATUS_DTYPE).reshape(-1)
+
+
+class DenseCode:
+    """Dense (non-reference) GF(2^8) codes, BASELINE config 5: caller-chosen coefficient matrices,
+    device Gauss-Jordan inversion (the work of detail::invert, invert_matrix.cc:9-128) and the
+    region MAC of attempt_full_decoding (detail/decoder.cc:503-534) for n up to 1024."""
+
+    def __init__(self, device: int | torch.device = 0):
+        self.engine = Engine.get(device)
+        self.device = self.engine.device
+
+    def encode(self, mat: torch.Tensor, src: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """rep[g][j] = sum_i mat[g][j][i] * src[g][i];  mat [G, r, k], src [G, k, stride]."""
+        G, k, stride = src.shape
+        r = mat.shape[1]
+        dev = self.device
+        _require(mat, "mat", _U8, (G, r, k), dev)
+        _require(src, "src", _U8, (G, k, stride), dev)
+        if out is None:
+            out = torch.empty((G, r, stride), dtype=torch.uint8, device=dev)
+        _require(out, "out", _U8, (G, r, stride), dev)
+        L = _native.load()
+        _native.check(L.ntc_gf256_dense_encode_batch(self.engine.handle, G, k, r, stride,
+                                                     mat.data_ptr(), src.data_ptr(),
+                                                     out.data_ptr(), _stream(dev)),
+                      "ntc_gf256_dense_encode_batch")
+        return out
+
+    def decode(self, mat: torch.Tensor, rep: torch.Tensor, out: torch.Tensor | None = None,
+               ok: torch.Tensor | None = None):
+        """(out, ok): out[g] = mat[g]^-1 rep[g];  ok[g] = 0 marks a singular matrix."""
+        G, n, stride = rep.shape
+        dev = self.device
+        _require(mat, "mat", _U8, (G, n, n), dev)
+        _require(rep, "rep", _U8, (G, n, stride), dev)
+        if out is None:
+            out = torch.empty((G, n, stride), dtype=torch.uint8, device=dev)
+        if ok is None:
+            ok = torch.empty((G,), dtype=torch.uint8, device=dev)
+        _require(out, "out", _U8, (G, n, stride), dev)
+        _require(ok, "ok", _U8, (G,), dev)
+        L = _native.load()
+        _native.check(L.ntc_gf256_dense_decode_batch(self.engine.handle, G, n, stride,
+                                                     mat.data_ptr(), rep.data_ptr(),
+                                                     out.data_ptr(), ok.data_ptr(), _stream(dev)),
+                      "ntc_gf256_dense_decode_batch")
+        return out, ok
+
+    def invert(self, mat: torch.Tensor):
+        """(inv, ok) for G n x n matrices."""
+        G, n, _ = mat.shape
+        dev = self.device
+        _require(mat, "mat", _U8, (G, n, n), dev)
+        inv = torch.empty((G, n, n), dtype=torch.uint8, device=dev)
+        ok = torch.empty((G,), dtype=torch.uint8, device=dev)
+        L = _native.load()
+        _native.check(L.ntc_gf256_dense_invert_batch(self.engine.handle, G, n, mat.data_ptr(),
+                                                     inv.data_ptr(), ok.data_ptr(), _stream(dev)),
+                      "ntc_gf256_dense_invert_batch")
+        return inv, ok

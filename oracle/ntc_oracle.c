@@ -96,6 +96,38 @@ static inline uint32_t gf_mul32(uint32_t x, uint32_t y)
   return (x == 0 || y == 0) ? 0 : g_mul[x & 0xFF][y & 0xFF];
 }
 
+/* Dense codes (config 5 extension): plain region MACs over a caller-chosen matrix. */
+void or_dense_encode(uint32_t k, uint32_t r, size_t stride, const uint8_t* mat, const uint8_t* src,
+                     uint8_t* rep)
+{
+  for (uint32_t j = 0; j < r; ++j) {
+    uint8_t* out = rep + (size_t)j * stride;
+    memset(out, 0, stride);
+    for (uint32_t i = 0; i < k; ++i)
+      if (mat[(size_t)j * k + i]) or_region_muladd(src + (size_t)i * stride, out, stride, mat[(size_t)j * k + i]);
+  }
+}
+
+long or_dense_decode(uint32_t n, size_t stride, const uint8_t* mat, const uint8_t* rep, uint8_t* out,
+                     uint8_t* inv)
+{
+  const size_t nn = (size_t)n * n;
+  uint32_t* m = (uint32_t*)malloc(nn * sizeof(uint32_t));
+  uint32_t* mi = (uint32_t*)malloc(nn * sizeof(uint32_t));
+  for (size_t e = 0; e < nn; ++e) m[e] = mat[e];
+  /* or_invert works on storage rows; the inverse of the row-major matrix comes out row-major */
+  const long fail = or_invert(m, mi, n);
+  memset(out, 0, (size_t)n * stride);
+  if (inv) for (size_t e = 0; e < nn; ++e) inv[e] = fail < 0 ? (uint8_t)mi[e] : 0;
+  if (fail < 0)
+    for (uint32_t t = 0; t < n; ++t)
+      for (uint32_t i = 0; i < n; ++i)
+        if (mi[(size_t)t * n + i]) or_region_muladd(rep + (size_t)i * stride, out + (size_t)t * stride, stride, (uint8_t)mi[(size_t)t * n + i]);
+  free(m);
+  free(mi);
+  return fail;
+}
+
 /* invert_matrix.cc:9-128 (jerasure_invert_matrix order; storage rows are matrix columns). */
 long or_invert(uint32_t* mat, uint32_t* inv, size_t n)
 {

@@ -35,6 +35,18 @@ uint16_t or_multiply_size(uint16_t size, uint32_t c);           /* galois_field.
  * Returns -1 on success, else the failure index the reference returns (rows-1). */
 long     or_invert(uint32_t* mat, uint32_t* inv, size_t n);
 
+/* ------------------------------------------------ dense codes (BASELINE config 5 extension) ---- */
+/* No reference counterpart beyond its building blocks: mat is a caller-chosen dense matrix (the
+ * reference's w=8 schedule makes k > 255 systems singular).  rep[j] = sum_i mat[j][i] * src[i]
+ * (mat [r][k] row-major, region MACs of galois_field.hh:83-92). */
+void or_dense_encode(uint32_t k, uint32_t r, size_t stride, const uint8_t* mat, const uint8_t* src,
+                     uint8_t* rep);
+/* out = mat^-1 * rep via or_invert (invert_matrix.cc:9-128) + region MACs (decoder.cc:503-534).
+ * Returns -1 on success, else or_invert's failure index (out and inv zeroed).  inv [n][n] row-major
+ * may be NULL. */
+long or_dense_decode(uint32_t n, size_t stride, const uint8_t* mat, const uint8_t* rep, uint8_t* out,
+                     uint8_t* inv);
+
 /* -------------------------------------------------------- generation encode (batch form) ---- */
 /* One generation: R_j = sum_i c(rid_base+j, sid_base+i) * X_i, sources zero padded to `stride`
  * (detail/encoder.cc:15-64).  src: [k][stride], rep: [r][stride]; rep_size[j] = encoded size. */

@@ -60,6 +60,10 @@ def lib():
         L.or_region_muladd_simd.argtypes = [P, P, C.c_size_t, C.c_uint8]
         L.or_invert.restype = C.c_long
         L.or_invert.argtypes = [P, P, C.c_size_t]
+        L.or_dense_encode.argtypes = [C.c_uint32, C.c_uint32, C.c_size_t, P, P, P]
+        L.or_dense_encode.restype = None
+        L.or_dense_decode.argtypes = [C.c_uint32, C.c_size_t, P, P, P, P]
+        L.or_dense_decode.restype = C.c_long
         L.or_encode_generation.argtypes = [C.c_uint32] * 3 + [P, P, C.c_uint32, C.c_uint32,
                                                               P, P, P]
         L.or_encode_batch.argtypes = [C.c_uint32] * 4 + [P, P, P, P, P, P, C.c_int, C.c_int]
@@ -135,6 +139,27 @@ def invert(mat_colmajor: np.ndarray):
     inv = np.zeros(n * n, np.uint32)
     r = lib().or_invert(_p(m), _p(inv), n)
     return (None if r < 0 else int(r)), inv
+
+
+def dense_encode(mat: np.ndarray, src: np.ndarray) -> np.ndarray:
+    """rep[j] = sum_i mat[j][i] * src[i]; mat [r][k] u8, src [k][stride]."""
+    r, k = mat.shape
+    stride = src.shape[1]
+    rep = np.zeros((r, stride), np.uint8)
+    lib().or_dense_encode(k, r, stride, _p(np.ascontiguousarray(mat, np.uint8)),
+                          _p(np.ascontiguousarray(src, np.uint8)), _p(rep))
+    return rep
+
+
+def dense_decode(mat: np.ndarray, rep: np.ndarray):
+    """(ok, out = mat^-1 rep, inv) for one dense n x n system."""
+    n = mat.shape[0]
+    stride = rep.shape[1]
+    out = np.zeros((n, stride), np.uint8)
+    inv = np.zeros((n, n), np.uint8)
+    f = lib().or_dense_decode(n, stride, _p(np.ascontiguousarray(mat, np.uint8)),
+                              _p(np.ascontiguousarray(rep, np.uint8)), _p(out), _p(inv))
+    return f < 0, out, inv
 
 
 # --------------------------------------------------------------------------- batch forms

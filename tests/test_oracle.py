@@ -160,3 +160,29 @@ def test_golden_fixtures_reproduce(oracle):
                                             z["sid_base"], z["rid_base"])
         assert (out == z["out"]).all() and (olen == z["out_len"]).all()
         assert (st.view(np.uint8).reshape(len(st), -1) == z["status"]).all()
+
+
+def test_dense_oracle_round_trip_and_inverse(oracle):
+    """Dense extension (config 5): or_dense_decode inverts with the reference's own invert
+    (invert_matrix.cc:9-128) -- M * M^-1 = I, decode(encode(x)) = x, singular reported."""
+    rng = np.random.default_rng(11)
+    T = oracle.mul_table()
+    for n in (1, 7, 48):
+        mat = rng.integers(0, 256, (n, n), dtype=np.uint8)
+        src = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+        ok, out, inv = oracle.dense_decode(mat, oracle.dense_encode(mat, src))
+        if not ok:
+            continue
+        assert (out == src).all()
+        prod = np.zeros((n, n), np.uint8)
+        for i in range(n):
+            for j in range(n):
+                acc = 0
+                for t in range(n):
+                    acc ^= int(T[mat[i, t], inv[t, j]])
+                prod[i, j] = acc
+        assert (prod == np.eye(n, dtype=np.uint8)).all()
+    mat = rng.integers(0, 256, (8, 8), dtype=np.uint8)
+    mat[3] = mat[1]
+    ok, out, inv = oracle.dense_decode(mat, np.zeros((8, 16), np.uint8))
+    assert not ok and not out.any() and not inv.any()

@@ -31,6 +31,8 @@ CONFIGS = {
     "k32r8s1024": (32, 8, 1024, 1024, 8, 4096),
     "k128r32s4096": (128, 32, 4096, 4096, 32, 4096),
     "k128r32s1500": (128, 32, 1500, 1504, 32, 8192),
+    # BASELINE configs[4] (extension): dense non-reference code, all k sources lost
+    "k1024dense": (1024, 1024, 65536, 65536, 1024, 1),
 }
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes/clk x 2.4 GHz
@@ -128,6 +130,56 @@ class Workload:
         return good, int(ok.sum().item())
 
 
+class DenseWorkload:
+    """BASELINE config 5: k = 1024 sources of 64 KiB, all lost; 1024 repairs from a seeded dense
+    random GF(2^8) matrix (re-drawn if singular).  Step = dense encode + dense decode (device
+    Gauss-Jordan of the 1024 x 1024 matrix + the MAC with its inverse)."""
+
+    def __init__(self, dev, G, k, S, rank):
+        from netcode_amd import DenseCode
+        self.dev, self.G, self.k, self.r, self.S, self.stride, self.m = dev, G, k, k, S, S, k
+        self.nlost = G * k
+        gen = torch.Generator(device=dev).manual_seed(4321 + rank)
+        self.src = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=gen)
+        self.dc = DenseCode(dev)
+        while True:
+            self.mat = torch.randint(0, 256, (G, k, k), dtype=torch.uint8, device=dev, generator=gen)
+            _, ok = self.dc.invert(self.mat)
+            if bool((ok != 0).all()):
+                break
+        self.rep = torch.empty((G, k, S), dtype=torch.uint8, device=dev)
+        self.out = torch.empty_like(self.src)
+        self.ok = torch.empty((G,), dtype=torch.uint8, device=dev)
+
+    def step(self):
+        self.dc.encode(self.mat, self.src, self.rep)
+        self.dc.decode(self.mat, self.rep, self.out, self.ok)
+
+    def kernel_times(self, reps=5):
+        s = torch.cuda.current_stream(self.dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        t_enc, t_inv, t_dec = [], [], []
+        for _ in range(reps):
+            ev[0].record(s)
+            self.dc.encode(self.mat, self.src, self.rep)
+            ev[1].record(s)
+            self.dc.invert(self.mat)
+            ev[2].record(s)
+            self.dc.decode(self.mat, self.rep, self.out, self.ok)
+            ev[3].record(s)
+            torch.cuda.synchronize(self.dev)
+            t_enc.append(ev[0].elapsed_time(ev[1]))
+            t_inv.append(ev[1].elapsed_time(ev[2]))
+            t_dec.append(ev[2].elapsed_time(ev[3]))
+        ti = float(np.mean(t_inv))
+        # decode = inversion + MAC with the inverse; report the MAC share as the apply time
+        return float(np.mean(t_enc)), ti, max(float(np.mean(t_dec)) - ti, 1e-6)
+
+    def verify(self):
+        good = bool((self.ok != 0).all().item()) and bool(torch.equal(self.out, self.src))
+        return good, int((self.ok != 0).sum().item())
+
+
 def host_rate(w, reps=3):
     """Pinned host -> device -> host round trip for the same step (PCIe-inclusive GiB/s)."""
     dev = w.dev
@@ -220,7 +272,12 @@ def main():
 
     import __graft_entry__
     __graft_entry__.build()
-    w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
+    dense = a.config == "k1024dense"
+    if dense:
+        w = DenseWorkload(dev, G, k, S, rank)
+        a.no_host_rate = a.no_cpu_baseline = True
+    else:
+        w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
 
     for _ in range(a.warmup):
         w.step()
@@ -290,7 +347,8 @@ def main():
                        "m": ("U[0,%d]" % m) if a.mixed else m, "generations_per_gpu": G,
                        "parallelism": f"generation-shard x{world} (no collectives)"},
             "roofline": roof,
-            "kernels_ms": {"encode_mac": round(t_enc, 4), "decode_plan": round(t_plan, 4),
+            "kernels_ms": {"encode_mac": round(t_enc, 4),
+                           ("dense_invert" if dense else "decode_plan"): round(t_plan, 4),
                            "decode_mac": round(t_apply, 4)},
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}
     if rank == 0 and world == 1 and not a.no_host_rate:

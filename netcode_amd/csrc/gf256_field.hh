@@ -71,6 +71,17 @@ constexpr PermTables make_perm_tables()
   return t;
 }
 
+// The same tables for the inverse of every coefficient (entry 0 stays all-zero): dividing by a
+// pivot is one lookup away.
+constexpr PermTables make_inv_perm_tables()
+{
+  PermTables t{};
+  const PermTables p = make_perm_tables();
+  for (int c = 1; c < 256; ++c)
+    for (int e = 0; e < 8; ++e) t.w[c][e] = p.w[field_inv(static_cast<uint8_t>(c))][e];
+  return t;
+}
+
 // netcode/detail/galois_field.hh:143-158 (w = 8): uint32 wraparound, then % 255 + 1.
 __host__ __device__ constexpr inline uint32_t coefficient(uint32_t repair_id, uint32_t src_id)
 {

@@ -32,15 +32,17 @@ namespace ntcgpu {
 namespace dense {
 
 __constant__ __attribute__((aligned(16))) PermTables dn_perm = make_perm_tables();
-__constant__ __attribute__((aligned(16))) FieldTables dn_field = make_field_tables();
+__constant__ __attribute__((aligned(16))) PermTables dn_pinv = make_inv_perm_tables();
 
 constexpr uint32_t kPanel = 32;       // pivot columns per panel
 constexpr uint32_t kMaxN = 1024;      // one thread per row in dn_panel
-constexpr int kUpdRows = 8;           // rows per wave in dn_update
-constexpr uint32_t kUpdSpan = 512;    // columns per wave in dn_update (64 lanes x 8 bytes)
+constexpr int kUpdRows = 4;           // rows per wave in dn_update
+constexpr uint32_t kUpdSpan = 256;    // columns per wave in dn_update (64 lanes x 4 bytes)
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
 // c*x for the four bytes of x; t = the 5 table dwords of c (PermTables layout, 3/3/2-bit split).
 __device__ __forceinline__ uint32_t mul4(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(256) void dn_init(const uint8_t* __restrict__ mat, 
 struct PanelArgs {
   uint32_t np, c0;
   const uint8_t* X;
-  uint8_t* W;          // [G][32][np] tracker, t-major
+  uint8_t* W;          // [G][np][32] tracker: row i's coefficients of the 32 pivot rows
   uint32_t* piv;       // [G][np] pivot row of column c
   uint8_t* flag;       // [G][np] 1 = not yet a pivot row (eligible)
   uint8_t* keep;       // [G][np] 0 = chosen as a pivot in this panel
@@ -91,19 +93,25 @@ struct PanelArgs {
 // its 32 tracker bytes.  At step t only dwords [t/4, 8) of the panel and [8, 8 + t/4] of the
 // tracker can be non-zero in a candidate row (earlier pivot columns are eliminated, later tracker
 // columns not yet assigned), so every step moves and multiplies exactly 9 dwords.
+// Step t: every wave with a candidate (eligible, non-zero in column t) takes its first one,
+// divides that row's window by its pivot value (tracker column t set: the row becomes pivot t) --
+// window dword e on lane e, gathered with readlane + select -- and publishes each dword with its
+// three v_perm selectors.  After the step's one barrier the lowest candidate is the pivot and
+// every other row subtracts f * (published window), f = its own column-t byte, whose table was
+// fetched before the barrier: 3 v_perm + 2 bitwise ops per dword.
 __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
 {
-  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
-  __shared__ uint8_t exp_t[512];
-  __shared__ uint8_t log_t[256];
+  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];   // tables of c
+  __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
   __shared__ uint32_t cmask[3];
   __shared__ uint32_t crow[2][16];
-  __shared__ __attribute__((aligned(16))) uint32_t cbuf[2][16][16];
+  __shared__ __attribute__((aligned(16))) u32x4 cbuf[2][16][9];     // {value, sel_a, sel_b, sel_e}
 
   const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
-  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
-  for (uint32_t e = i; e < 512; e += blockDim.x) exp_t[e] = dn_field.exp[e];
-  for (uint32_t e = i; e < 256; e += blockDim.x) log_t[e] = dn_field.log[e];
+  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) {
+    perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+    pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
+  }
   if (i < 3) cmask[i] = 0;
   const bool live = a.ok[g] != 0;
   __syncthreads();
@@ -131,17 +139,37 @@ __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
 #pragma unroll
   for (int t = 0; t < static_cast<int>(kPanel); ++t) {
     const int q = t >> 2, sh = 8 * (t & 3), par = t & 1;
+    // window entry e -> row dword: panel dwords q..7, then tracker dwords 8..8+q
+    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
     const uint32_t f = (v[q] >> sh) & 0xFFu;
+    const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);   // f = 0: all-zero table
+    const uint32_t tf4 = perm_t[f][4];
     const uint64_t b = __ballot(elig && f != 0);
-    if (b != 0 && lane == static_cast<uint32_t>(__ffsll(static_cast<long long>(b)) - 1)) {
-      // this wave's candidate: publish its live window with tracker column t set (the row in the
-      // pivot basis: it stops counting as itself and becomes pivot t)
+    if (b != 0) {                                      // wave-uniform
+      const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
+      uint32_t x = 0;
 #pragma unroll
-      for (int d = q; d < 8; ++d) cbuf[par][w][d] = v[d];
-#pragma unroll
-      for (int d = 8; d <= 8 + q; ++d) cbuf[par][w][d] = v[d] ^ (d == 8 + q ? (1u << sh) : 0u);
-      crow[par][w] = i;
-      atomicOr(&cmask[t % 3], 1u << w);
+      for (int e = 0; e < 9; ++e) {
+        uint32_t val = __builtin_amdgcn_readlane(v[wd(e)], first);
+        if (wd(e) == 8 + q) val ^= 1u << sh;
+        x = lane == static_cast<uint32_t>(e) ? val : x;
+      }
+      const uint32_t fc = __builtin_amdgcn_readlane(f, first);
+      const u32x4 ti = *reinterpret_cast<const u32x4*>(&pinv_t[fc][0]);
+      const uint32_t ti4 = pinv_t[fc][4];
+      if (lane < 9) {
+        const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
+        u32x4 o;
+        o[0] = nv;
+        o[1] = nv & 0x07070707u;
+        o[2] = (nv >> 3) & 0x07070707u;
+        o[3] = (nv >> 6) & 0x03030303u;
+        cbuf[par][w][lane] = o;
+      }
+      if (lane == 0) {
+        crow[par][w] = w * 64u + first;
+        atomicOr(&cmask[t % 3], 1u << w);
+      }
     }
     __syncthreads();
     const uint32_t m = cmask[t % 3];
@@ -149,28 +177,20 @@ __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
     if (m == 0) { singular = true; break; }            // uniform
     const uint32_t ws = __ffs(m) - 1;                  // lowest wave = lowest row index
     const uint32_t prow = crow[par][ws];
-    const uint32_t pv = (cbuf[par][ws][q] >> sh) & 0xFFu;
-    const uint32_t lpv = log_t[pv];
-    uint32_t c = 0;
+    if (i == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + t] = prow;
     if (i == prow) {
-      c = exp_t[255 - lpv];                            // 1 / pivot (pv != 0)
       chosen = true;
       elig = false;
 #pragma unroll
-      for (int d = q; d < 8; ++d) v[d] = 0;
-#pragma unroll
-      for (int d = 8; d <= 8 + q; ++d) v[d] = 0;
+      for (int e = 0; e < 9; ++e) v[wd(e)] = cbuf[par][ws][e][0];
     } else if (f != 0) {
-      c = exp_t[log_t[f] + 255 - lpv];                 // f / pivot
-    }
-    if (i == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + t] = prow;
-    if (c != 0) {
-      const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
-      const uint32_t t4 = perm_t[c][4];
 #pragma unroll
-      for (int d = q; d < 8; ++d) v[d] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, cbuf[par][ws][d]);
-#pragma unroll
-      for (int d = 8; d <= 8 + q; ++d) v[d] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, cbuf[par][ws][d]);
+      for (int e = 0; e < 9; ++e) {
+        const u32x4 c4 = cbuf[par][ws][e];
+        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                               __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
+                   __builtin_amdgcn_perm(tf4, tf4, c4[3]);
+      }
     }
   }
   if (singular) {
@@ -180,10 +200,12 @@ __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
   if (row_ok) {
     a.flag[gi] = elig ? 1 : 0;
     a.keep[gi] = chosen ? 0 : 1;
-    uint8_t* wg = a.W + static_cast<size_t>(g) * kPanel * np + i;
-#pragma unroll
-    for (int t = 0; t < static_cast<int>(kPanel); ++t)
-      wg[static_cast<size_t>(t) * np] = static_cast<uint8_t>(v[8 + (t >> 2)] >> (8 * (t & 3)));
+    u32x4* wg = reinterpret_cast<u32x4*>(a.W + gi * kPanel);
+    u32x4 o0, o1;
+    o0[0] = v[8]; o0[1] = v[9]; o0[2] = v[10]; o0[3] = v[11];
+    o1[0] = v[12]; o1[1] = v[13]; o1[2] = v[14]; o1[3] = v[15];
+    wg[0] = o0;
+    wg[1] = o1;
   }
 }
 
@@ -198,10 +220,16 @@ struct UpdArgs {
   const uint8_t* ok;
 };
 
-// One wave per (generation, 8-row tile, 512-column span of [cs, 2np)):
+// One wave per (generation, 4-row tile, 256-column span of [cs, 2np)), 4 bytes per lane:
 //   Y[i][c] = keep_i * X[i][c]  XOR  sum_t W[t][i] * X[piv_t][c]
+// Pivot-row slices stream in groups of 8 with the next group's loads in flight; v_perm tables come
+// from an LDS copy (uniform addresses: broadcast reads).  Narrow spans keep >= 2 waves per SIMD
+// at n = 1024 (G = 1), which this latency-bound kernel needs.
 __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
 {
+  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
+  for (uint32_t e = threadIdx.x; e < 256 * 8; e += 256) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t span = task % a.nspans;
@@ -211,53 +239,60 @@ __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
   if (g >= a.G) return;
   if (__builtin_amdgcn_readfirstlane(a.ok[g]) == 0) return;
   const uint32_t np = a.np, P = 2 * np;
-  const uint32_t col = a.cs + span * kUpdSpan + lane * 8u;
+  const uint32_t col = a.cs + span * kUpdSpan + lane * 4u;
   const bool active = col < P;
   const uint32_t cx = active ? col : a.cs;
-  const uint8_t* Xg = a.X + static_cast<size_t>(g) * np * P;
+  const uint8_t* Xg = a.X + static_cast<size_t>(g) * np * P + cx;
   uint8_t* Yg = a.Y + static_cast<size_t>(g) * np * P;
   const uint32_t i0 = tile * kUpdRows;
-  const uint8_t* keep = a.keep + static_cast<size_t>(g) * np + i0;
   const uint32_t* piv = a.piv + static_cast<size_t>(g) * np + a.c0;
-  const uint8_t* Wg = a.W + static_cast<size_t>(g) * kPanel * np + i0;
+  // the tile's 4 x 32 tracker bytes: byte t of row j = word 8j + t/4, all in SGPRs up front
+  const u32x16 w0 = const_load<u32x16>(a.W + (static_cast<size_t>(g) * np + i0) * kPanel);
+  const u32x16 w1 = const_load<u32x16>(a.W + (static_cast<size_t>(g) * np + i0) * kPanel + 64);
 
-  uint32_t acc[kUpdRows][2];
-  const u32x2 kw = const_load<u32x2>(keep);
+  const uint32_t kw = const_load<uint32_t>(a.keep + static_cast<size_t>(g) * np + i0);
+  uint32_t acc[kUpdRows];
 #pragma unroll
-  for (int j = 0; j < kUpdRows; ++j) {
-    const uint32_t kj = (kw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-    if (kj) {
-      const u32x2 x = *reinterpret_cast<const u32x2*>(Xg + static_cast<size_t>(i0 + j) * P + cx);
-      acc[j][0] = x[0];
-      acc[j][1] = x[1];
-    } else {
-      acc[j][0] = acc[j][1] = 0;
-    }
+  for (int j = 0; j < kUpdRows; ++j)
+    acc[j] = ((kw >> (8 * j)) & 0xFFu) ? *reinterpret_cast<const uint32_t*>(Xg + static_cast<size_t>(i0 + j) * P) : 0u;
+  constexpr uint32_t kGrp = 8;
+  uint32_t xc[kGrp];
+  {
+    const u32x8 pg = const_load<u32x8>(piv);
+#pragma unroll
+    for (uint32_t u = 0; u < kGrp; ++u) xc[u] = *reinterpret_cast<const uint32_t*>(Xg + static_cast<size_t>(pg[u]) * P);
   }
-#pragma unroll 4
-  for (uint32_t t = 0; t < kPanel; ++t) {
-    const uint32_t prow = const_load<uint32_t>(piv + t);
-    const u32x2 x = *reinterpret_cast<const u32x2*>(Xg + static_cast<size_t>(prow) * P + cx);
-    const u32x2 cw = const_load<u32x2>(Wg + static_cast<size_t>(t) * np);
 #pragma unroll
-    for (int j = 0; j < kUpdRows; ++j) {
-      const uint32_t c = (cw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-      if (c) {
-        const u32x4 tab = const_load<u32x4>(&dn_perm.w[c][0]);
-        const uint32_t t4 = const_load<uint32_t>(&dn_perm.w[c][4]);
-        acc[j][0] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, x[0]);
-        acc[j][1] ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, x[1]);
+  for (uint32_t grp = 0; grp < kPanel / kGrp; ++grp) {
+    uint32_t xn[kGrp];
+    if (grp + 1 < kPanel / kGrp) {
+      const u32x8 pg = const_load<u32x8>(piv + kGrp * (grp + 1));
+#pragma unroll
+      for (uint32_t u = 0; u < kGrp; ++u) xn[u] = *reinterpret_cast<const uint32_t*>(Xg + static_cast<size_t>(pg[u]) * P);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kGrp; ++u) {
+      const uint32_t t = kGrp * grp + u;
+      const uint32_t sa = xc[u] & 0x07070707u, sb = (xc[u] >> 3) & 0x07070707u, se = (xc[u] >> 6) & 0x03030303u;
+#pragma unroll
+      for (int j = 0; j < kUpdRows; ++j) {
+        const uint32_t wi = 8u * j + (t >> 2);
+        const uint32_t c = ((wi < 16 ? w0[wi & 15] : w1[wi & 15]) >> (8 * (t & 3))) & 0xFFu;   // 0: zero table
+        const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
+        const uint32_t t4 = perm_t[c][4];
+        acc[j] = __builtin_amdgcn_bitop3_b32(acc[j], __builtin_amdgcn_perm(tab[1], tab[0], sa),
+                                             __builtin_amdgcn_perm(tab[3], tab[2], sb), 0x96) ^
+                 __builtin_amdgcn_perm(t4, t4, se);
       }
+    }
+    if (grp + 1 < kPanel / kGrp) {
+#pragma unroll
+      for (uint32_t u = 0; u < kGrp; ++u) xc[u] = xn[u];
     }
   }
   if (!active) return;
 #pragma unroll
-  for (int j = 0; j < kUpdRows; ++j) {
-    u32x2 o;
-    o[0] = acc[j][0];
-    o[1] = acc[j][1];
-    *reinterpret_cast<u32x2*>(Yg + static_cast<size_t>(i0 + j) * P + col) = o;
-  }
+  for (int j = 0; j < kUpdRows; ++j) *reinterpret_cast<uint32_t*>(Yg + static_cast<size_t>(i0 + j) * P + col) = acc[j];
 }
 
 // inv[g][t][0..n) = X[g][piv[t]][np .. np + n)  (zeros for a singular generation)

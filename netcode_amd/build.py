@@ -54,5 +54,50 @@ def build(force: bool = False, verbose: bool = True) -> list[str]:
     return built
 
 
+# C++ surface checks (tests/, not product): our own driver of include/netcode/*.hh, and -- when
+# the reference tree is present (this container only) -- the reference's own public-API programs
+# compiled unmodified against our headers and libntc.so.  Outputs go to tests/_build/ (git-ignored,
+# shipped to the GPU box with the tree).
+REF = "/root/reference"
+CPP_CHECKS = {
+    "cpp_surface_test": ("tests/cpp/cpp_surface_test.cc", False),
+    "ref_cpp_basic": (REF + "/examples/basic/cpp_basic.cc", True),
+    "ref_c_basic": (REF + "/examples/basic/c_basic.c", True),
+    "ref_end_to_end": (REF + "/tests/end_to_end.cc", True),
+}
+
+
+def build_cpp_checks(verbose: bool = True) -> list[str]:
+    out_dir = os.path.join(ROOT, "tests", "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    lib_dir = HERE
+    built = []
+    for name, (src, is_ref) in CPP_CHECKS.items():
+        src_p = src if os.path.isabs(src) else os.path.join(ROOT, src)
+        if not os.path.exists(src_p):
+            continue
+        out = os.path.join(out_dir, name)
+        deps = [src_p, os.path.join(HERE, "libntc.so")]
+        for d in ("include/netcode", "include/netcode/detail", "include/netcode/c"):
+            dd = os.path.join(ROOT, d)
+            deps += [os.path.join(dd, f) for f in os.listdir(dd)]
+        if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps if os.path.exists(d)):
+            built.append(out)
+            continue
+        c = src_p.endswith(".c")
+        cmd = ["gcc" if c else "g++", "-std=c11" if c else "-std=c++11", "-O2", "-Wall",
+               "-I", os.path.join(ROOT, "include")]
+        if is_ref:
+            cmd += ["-I", REF]          # only for the reference's own test helpers (tools/loss)
+        cmd += ["-o", out, src_p, "-L", lib_dir, "-lntc", "-lntc_gf256",
+                "-Wl,-rpath," + os.path.relpath(lib_dir, out_dir).join(["$ORIGIN/", ""])]
+        if verbose:
+            print("[netcode_amd.build]", " ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        built.append(out)
+    return built
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_cpp_checks()

@@ -1,0 +1,37 @@
+"""CPU checks of the header-only C++ surface (include/netcode/{encoder,decoder,packet,data,
+errors,dispatch}.hh over libntc.so): it compiles under -std=c++11 with our own driver and -- where
+the reference tree is present -- the reference's own public-API programs (examples/basic/
+cpp_basic.cc, c_basic.c, tests/end_to_end.cc) compile and link unmodified against it.  Without a
+HIP device the programs fail loudly (no CPU fallback)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "tests", "_build")
+
+
+@pytest.fixture(scope="module")
+def cpp_checks(native_built):
+    from netcode_amd import build
+    return {os.path.basename(p): p for p in build.build_cpp_checks(verbose=False)}
+
+
+def test_own_driver_compiles(cpp_checks):
+    assert "cpp_surface_test" in cpp_checks
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="reference tree not present")
+def test_reference_programs_compile_against_our_headers(cpp_checks):
+    for name in ("ref_cpp_basic", "ref_c_basic", "ref_end_to_end"):
+        assert name in cpp_checks, name
+
+
+def test_no_device_fails_loudly(cpp_checks):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    r = subprocess.run([cpp_checks["cpp_surface_test"], "10"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert "no MI355X engine" in r.stderr

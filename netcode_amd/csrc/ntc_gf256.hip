@@ -348,13 +348,13 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
 // ---- bit-sliced MAC: jump-chained XOR blocks ---------------------------------------------------
 // A lane owns 32 bytes = 8 dwords.  transpose8 turns them into 8 bit-planes (plane p = bit p of
 // every byte; an involution, so the same code slices and un-slices).  Multiplication by c is then
-// linear over GF(2): c*x = sum_t c_t (alpha^t x), with y_t = alpha^t x built per source by the
-// xtime recurrence (29 distinct planes).  Each (row, coefficient nibble) "site" is a table of 16
-// fixed-size blocks of v_xor/v_bitop3 (gf_bitslice_chain.inc, generated by
-// tools/gen_bitslice_chain.py); a source's 2R sites run as a chain of s_setpc jumps whose block
-// offsets bj_offsets precomputed from the coefficient matrix.  Per (source, row) that is ~20
-// full-rate VALU ops for 32 bytes plus 6 scalar ops, against 24 half-rate v_perm + 12 XOR for
-// the byte-domain kernel.
+// linear over GF(2): plane p of c*x is an XOR of input planes.  Per source the XOR combinations
+// of planes 0-3 and of planes 4-7 are built once (Four-Russians tables, 30 planes); each
+// (row, coefficient nibble) "site" is a table of 16 fixed-size blocks of one v_bitop3 per output
+// plane (gf_bitslice_chain.inc, generated by tools/gen_bitslice_chain.py); a source's 2R sites
+// run as a chain of s_setpc jumps whose block offsets bj_offsets precomputed from the coefficient
+// matrix.  Per (source, row) that is 15 full-rate VALU ops for 32 bytes plus 4 scalar ops,
+// against 24 half-rate v_perm + 12 XOR for the byte-domain kernel.
 #include "gf_bitslice_chain.inc"
 
 // Delta swap of the `mask` bit groups of b with the groups `sh` bits higher in a: two shifts and
@@ -467,7 +467,7 @@ __device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, ui
 }
 
 // ABL != 0: timing ablations of the encode kernel (NTC_GF256_BJ_ABLATE; results are wrong):
-// 1 no transpose, 2 no xtime, 4 straight-line stand-in for the chain, 8 no chain.
+// 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain.
 template <int R, int RT, bool DEC, int ABL = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
@@ -551,7 +551,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
     for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + static_cast<size_t>(i1) * jstep + 16 * h);
     if constexpr (!(ABL & 2)) {
-      NTC_BJ_XTIME(Y)
+      NTC_BJ_TABLES(Y)
     } else {
 #pragma unroll
       for (int n = 8; n < kBjPlanes; ++n) Y[n] = Y[n & 7] + n;
@@ -564,8 +564,8 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
       for (int j = 0; j < R; ++j)
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
-          acc[j][p] = bxor3(acc[j][p], Y[(j + p) % 29], Y[(j + 2 * p + 3) % 29]);
-          acc[j][p] = bxor3(acc[j][p], Y[(3 * j + p + 7) % 29], O[(j + p) & 15]);
+          acc[j][p] = bxor3(acc[j][p], Y[(j + p) % kBjPlanes], Y[(j + 2 * p + 3) % kBjPlanes]);
+          acc[j][p] = bxor3(acc[j][p], Y[(3 * j + p + 7) % kBjPlanes], O[(j + p) & 15]);
         }
       continue;
     }

@@ -1,17 +1,21 @@
 """Generate netcode_amd/csrc/gf_bitslice_chain.inc — the jump-chained bit-sliced MAC block tables.
 
 Bit-sliced GF(2^8) multiply-accumulate: a lane holds 32 bytes as 8 bit-planes
-x_0..x_7; y_t = alpha^t * x (t = 0..7) are 8-plane values built by the xtime recurrence for the
-field polynomial 0x11D (x^8 = x^4 + x^3 + x^2 + 1), so only 3 planes per step are new: 29
-distinct planes Y[0..28] in all.  c * x = XOR_{t in bits(c)} y_t.
+x_0..x_7.  Multiplication by a constant m is GF(2)-linear: plane p of m*x is the XOR of the input
+planes q whose bit p of m*alpha^q is set.  Four-Russians split: per source the 15 non-empty XOR
+combinations of planes 0-3 (TL) and of planes 4-7 (TH) are built once (22 XORs; singletons are the
+planes themselves), 30 distinct planes Y[0..29] in all; then every output plane of m*x is
+TL[a_p] ^ TH[b_p] -- one 3-input v_bitop3 (or one v_xor when a half is empty).
 
-For a row tile of R rows one source contributes to 2R "sites" (row j, coefficient nibble h).
-Each site owns 16 blocks (one per nibble value v) that XOR the selected y planes into the row's
-8 accumulator planes, then jump to the next site's block: the per-source dispatch is a chain of
+For a row tile of R rows one source contributes to 2R "sites" (row j, coefficient nibble h): the
+low nibble multiplies x by v, the high nibble by v*alpha^4 (c*x = lo(c)*x ^ hi(c)*(alpha^4 x)).
+Each site owns 16 blocks (one per nibble value v) of at most 8 ops that XOR into the row's 8
+accumulator planes, then jump to the next site's block: the per-source dispatch is a chain of
 2R `s_setpc_b64`, with the block offsets of every (source, site) precomputed on the device
-(`bj_offsets` kernel: offset = site * kBjSite + kBjVo[v]).  Block sizes depend only on popcount(v)
-(8 VOP2 or VOP3 per XOR round); `.fill` pads every block to exactly its table size, so an
-encoding that grew would be an assembler error, never a silent misjump.
+(`bj_offsets` kernel: offset = site * kBjSite + kBjVo[v]).  `.fill` pads every block to exactly
+its table size, so an encoding that grew would be an assembler error, never a silent misjump.
+(Full 256-entry Four-Russians blocks per row would halve the ops again, but 8 rows x 20 KiB of
+code thrash the instruction cache: tools/gen_microbench_fr.py.)
 
 Two copies of the tables share one asm statement and one layout: the fast chain keeps the high
 half of the jump target fixed (s_add + s_setpc per site); if the fast tables straddle a 4 GiB
@@ -28,58 +32,83 @@ OUT = os.environ.get("NTC_BJ_OUT") or os.path.join(os.path.dirname(HERE), "netco
 TILES = (16, 8, 4)
 
 
-def popcount(v):
-    return bin(v).count("1")
+NPLANES = 30
 
 
-def valu_bytes(v):
-    return {0: 0, 1: 32, 2: 64, 3: 96, 4: 128}[popcount(v)]
+def gmul(a, b):
+    """GF(2^8) product, polynomial 0x11D."""
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        a <<= 1
+        if a & 0x100:
+            a ^= 0x11D
+        b >>= 1
+    return r
+
+
+def table_planes():
+    """lo[v] / hi[v]: index in Y of the XOR of input planes {q in v} (q < 4) / {4 + q}; the C++
+    statements that build the 22 composite planes Y[8..29] from Y[0..7]."""
+    lo, hi = [None] * 16, [None] * 16
+    stmts, n = [], 8
+    for half, tab in ((0, lo), (4, hi)):
+        for q in range(4):
+            tab[1 << q] = half + q
+        for v in range(3, 16):
+            if v & (v - 1):
+                low = v & -v
+                stmts.append(f"Y[{n}] = Y[{tab[v ^ low]}] ^ Y[{tab[low]}];")
+                tab[v] = n
+                n += 1
+    assert n == NPLANES
+    return lo, hi, stmts
+
+
+def nibble_ops(lo, hi, m, j):
+    """acc[j] ^= m * x: per output plane p, TL[a_p] ^ TH[b_p] with (a_p, b_p) the two nibbles of
+    row p of m's 8x8 GF(2) matrix (column q = m * alpha^q)."""
+    cols = [gmul(m, 1 << q) for q in range(8)]
+    ops = []
+    for p in range(8):
+        a = sum(((cols[q] >> p) & 1) << q for q in range(4))
+        b = sum(((cols[4 + q] >> p) & 1) << q for q in range(4))
+        acc = f"%[a{j}_{p}]"
+        if a and b:
+            ops.append(f"v_bitop3_b32 {acc}, {acc}, %[y{lo[a]}], %[y{hi[b]}] bitop3:0x96")
+        elif a or b:
+            ops.append(f"v_xor_b32_e32 {acc}, %[y{lo[a] if a else hi[b]}], {acc}")
+    return ops
+
+
+def block_bytes(ops):
+    return sum(8 if o.startswith("v_bitop3") else 4 for o in ops)
+
+
+def block_body(planes, j, h, v):
+    lo, hi = planes
+    if v == 0:
+        return []
+    return nibble_ops(lo, hi, v if h == 0 else gmul(v, 16), j)
 
 
 TAIL = 12      # s_add [+ s_addc] + s_setpc
 ALIGN = int(os.environ.get("NTC_BJ_ALIGN", "16"))   # every block starts ALIGN-byte aligned
-SIZES = [(valu_bytes(v) + TAIL + ALIGN - 1) // ALIGN * ALIGN for v in range(16)]
+
+
+def _sizes():
+    lo, hi, _ = table_planes()
+    need = [0] * 16
+    for h in range(2):
+        for v in range(16):
+            need[v] = max(need[v], block_bytes(block_body((lo, hi), 0, h, v)))
+    return [(n + TAIL + ALIGN - 1) // ALIGN * ALIGN for n in need]
+
+
+SIZES = _sizes()
 VO = [sum(SIZES[:v]) for v in range(16)]
 SITE = sum(SIZES)
-
-
-def xtime_planes():
-    """y[t][p] -> index into the distinct-plane list Y, plus the C++ statements that build Y."""
-    y = [list(range(8))]
-    stmts, n = [], 8
-    for t in range(1, 8):
-        u = y[-1]
-        nxt = [u[7], u[0], None, None, None, u[4], u[5], u[6]]
-        for p, src in ((2, 1), (3, 2), (4, 3)):
-            stmts.append(f"Y[{n}] = Y[{u[src]}] ^ Y[{u[7]}];")
-            nxt[p] = n
-            n += 1
-        y.append(nxt)
-    assert n == 29
-    return y, stmts
-
-
-def block_body(y, j, h, v):
-    """Instructions for acc[j] ^= sum_{t in bits(v)} y[4h + t], interleaved across planes."""
-    ts = [4 * h + t for t in range(4) if v >> t & 1]
-    rounds = []
-    for p in range(8):
-        regs = [f"%[y{y[t][p]}]" for t in ts]
-        acc = f"%[a{j}_{p}]"
-        ops = []
-        if len(regs) == 1:
-            ops.append(f"v_xor_b32_e32 {acc}, {regs[0]}, {acc}")
-        elif len(regs) >= 2:
-            ops.append(f"v_bitop3_b32 {acc}, {acc}, {regs[0]}, {regs[1]} bitop3:0x96")
-            if len(regs) == 3:
-                ops.append(f"v_xor_b32_e32 {acc}, {regs[2]}, {acc}")
-            elif len(regs) == 4:
-                ops.append(f"v_bitop3_b32 {acc}, {acc}, {regs[2]}, {regs[3]} bitop3:0x96")
-        rounds.append(ops)
-    out = []
-    for k in range(2):                       # first op of every plane, then the second ones
-        out += [r[k] for r in rounds if len(r) > k]
-    return out
 
 
 def tables(y, R, safe):
@@ -125,16 +154,17 @@ def chain_lines(y, R):
 
 
 def main():
-    y, stmts = xtime_planes()
+    lo, hi, stmts = table_planes()
+    y = (lo, hi)
     o = ["// Generated by tools/gen_bitslice_chain.py -- do not edit by hand.",
          "// Jump-chained bit-sliced GF(2^8) MAC blocks (see the generator's docstring).",
          "#pragma once", "",
          f"constexpr uint32_t kBjSite = {SITE};          // bytes per site (16 nibble blocks)",
          "// byte offset of nibble value v's block inside a site",
          "__device__ constexpr uint32_t kBjVo[16] = {" + ", ".join(map(str, VO)) + "};",
-         "constexpr int kBjPlanes = 29;                   // distinct planes of y_0..y_7", "",
-         "// Y[8..28] from the bit-planes Y[0..7]: y_t = alpha^t x for the polynomial 0x11D.",
-         "#define NTC_BJ_XTIME(Y) \\"]
+         f"constexpr int kBjPlanes = {NPLANES};                   // input planes + their XOR combinations", "",
+         "// Y[8..29]: the XOR combinations of input planes 0-3 and 4-7 (Four-Russians tables).",
+         "#define NTC_BJ_TABLES(Y) \\"]
     o += [f"  {st} \\" for st in stmts]
     o.append("")
     for R in TILES:
@@ -143,7 +173,7 @@ def main():
         o.append("")
         outs = ", ".join(f'[a{j}_{p}] "+v"(A[{j}][{p}])' for j in range(R) for p in range(8))
         o.append(f"#define NTC_BJ_OUTS_R{R}(A) {outs}")
-        ins = ", ".join(f'[y{n}] "v"(Y[{n}])' for n in range(29))
+        ins = ", ".join(f'[y{n}] "v"(Y[{n}])' for n in range(NPLANES))
         ins += ", " + ", ".join(f'[o{s}] "s"(O[{s}])' for s in range(2 * R))
         o.append(f"#define NTC_BJ_INS_R{R}(Y, O) {ins}")
         o.append("")

@@ -10,5 +10,5 @@ timeout -k 10 300 python bench.py > gpurun_out/$TAG/bench.log 2>&1 || { tail -20
 tail -1 gpurun_out/$TAG/bench.log
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/$TAG
-(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 $OLDPWD/bench.py --steps 10 --no-cpu-baseline --no-host-rate > $OUT/prof_bench.log 2>&1) || { tail -20 $OUT/prof_bench.log; exit 1; }
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- python3 $OLDPWD/bench.py --steps 10 --no-cpu-baseline --no-host-rate > $OUT/prof_bench.log 2>&1) || { tail -20 $OUT/prof_bench.log; exit 1; }
 find $OUT/prof -name "*kernel_stats.csv" | head -3

@@ -742,45 +742,33 @@ __device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
 }
 
 
-// D rows for four received-source positions (one lane): acc[s] holds D[s][p0..p0+3] as bytes.
+// D column of one received-source position j (one lane): D[s][j] = sum_q (M^-1)[s][q] * c(q, j)
+// for the R (padded) output rows s.  The lane's coefficient c(q, j) selects its own v_perm table
+// (one 32-byte row of d_perm per q); the wave-uniform bytes (M^-1)[s..s+3][q] are the data, so one
+// mul4 yields four rows' products.  acc[w] = D[4w..4w+3][j], the byte order of the plan's
+// position-major layout (pc[j][s]).
 template <int R, int RM>
-__device__ __forceinline__ void plan_dmac(uint32_t m, uint32_t p0, uint32_t nb, uint32_t sidb,
-                                          const uint16_t* rl, const uint32_t* rq1,
-                                          const uint16_t (*mA)[RM], uint8_t* dst, uint32_t rp)
+__device__ __forceinline__ void plan_dcol(uint32_t m, uint32_t j, uint32_t sidb,
+                                          const uint32_t* rq1, const uint32_t (*minvT)[RM / 4],
+                                          uint8_t* dst, uint32_t rp)
 {
-  uint32_t S1[4];
+  const uint32_t S1 = sidb + j + 1u;
+  uint32_t acc[R / 4];
 #pragma unroll
-  for (int b = 0; b < 4; ++b) S1[b] = sidb + rl[p0 + (static_cast<uint32_t>(b) < nb ? b : 0)] + 1u;
-  uint32_t acc[R];
-#pragma unroll
-  for (int t = 0; t < R; ++t) acc[t] = 0;
+  for (int w = 0; w < R / 4; ++w) acc[w] = 0;
   for (uint32_t q = 0; q < m; ++q) {
     const uint32_t R1 = rq1[q];
-    uint32_t x = 0;
+    const uint32_t c = ((R1 + S1) * R1) % 255u + 1u;   // galois_field.hh:143-158
+    const uint4 ab = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);
+    const uint32_t tf[5] = {ab.x, ab.y, ab.z, ab.w, d_perm.w[c][4]};
 #pragma unroll
-    for (int b = 0; b < 4; ++b) x |= ((((R1 + S1[b]) * R1) % 255u) + 1u) << (8 * b);
-    const uint32_t sa = x & 0x07070707u, sb = (x >> 3) & 0x07070707u, se = (x >> 6) & 0x03030303u;
-    const uint16_t* row = mA[q];
-#pragma unroll
-    for (int t = 0; t < R; ++t) {
-      const uint32_t* tb = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&d_perm.w[0][0]) + row[t]);
-      const uint4 ab = *reinterpret_cast<const uint4*>(tb);
-      const uint32_t e = tb[4];
-      acc[t] ^= xor3(__builtin_amdgcn_perm(ab.y, ab.x, sa), __builtin_amdgcn_perm(ab.w, ab.z, sb),
-                     __builtin_amdgcn_perm(e, e, se));
-    }
+    for (int w = 0; w < R / 4; ++w) acc[w] ^= mul4(tf, minvT[q][w]);
   }
-  for (uint32_t b = 0; b < nb; ++b) {
-    uint8_t* d = dst + b * rp;
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);      // rp is a multiple of 4
 #pragma unroll
-    for (int t = 0; t < R; t += 4) {
-      const uint32_t w = ((acc[t] >> (8 * b)) & 0xFFu) | (((acc[t + 1] >> (8 * b)) & 0xFFu) << 8) |
-                         (((acc[t + 2] >> (8 * b)) & 0xFFu) << 16) | (((acc[t + 3] >> (8 * b)) & 0xFFu) << 24);
-      if (static_cast<uint32_t>(t) < rp) *reinterpret_cast<uint32_t*>(d + t) = w;
-    }
-    for (uint32_t t = R; t < rp; t += 4) *reinterpret_cast<uint32_t*>(d + t) = 0;
-  }
-  (void)m;
+  for (int w = 0; w < R / 4; ++w)
+    if (4u * w < rp) d[w] = acc[w];
+  for (uint32_t t = R; t < rp; t += 4) d[t / 4] = 0;
 }
 
 // RM = row bound of this instantiation (r <= RM): sizes LDS and registers to the launch, so
@@ -796,7 +784,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   __shared__ uint16_t miss[RM];
   __shared__ uint16_t recv[RM];
   __shared__ uint16_t reps[RM];
-  __shared__ uint16_t mA[RM][RM];              // 32 * (M^-1)[s][q], [q][s]
+  __shared__ uint32_t minvT[RM][RM / 4];       // (M^-1)[s][q] bytes, [q][s]
   __shared__ uint32_t rq1[RM];
   __shared__ uint16_t rl[kChunk];
   __shared__ uint16_t sl[kChunk];
@@ -812,13 +800,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
     if (lane < 32) reinterpret_cast<uint4*>(exp_t)[lane] = ve;
     else if (lane < 48) reinterpret_cast<uint4*>(log_t)[lane - 32] = ve;
   }
-  // galois_field::multiply_size (galois_field.hh:108-115) on the LDS tables
-  auto msize = [&](uint32_t size, uint32_t c) -> uint32_t {
-    if (size == 0 || c == 0) return 0u;
-    const uint32_t lc = log_t[c];
-    const uint32_t lo = size & 0xFFu, hi = size >> 8;
-    return (lo ? exp_t[log_t[lo] + lc] : 0u) | ((hi ? exp_t[log_t[hi] + lc] : 0u) << 8);
-  };
+
 
   const uint32_t k = a.k, r = a.r;
   const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
@@ -952,9 +934,12 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         szs[lane] = rszL[reps[lane]];           // becomes the reduced encoded size of repair q
       }
       const uint32_t R = m <= 8 ? 8u : m <= 16 ? 16u : m <= 32 ? 32u : 64u;   // <= RM
-      for (uint32_t idx = lane; idx < m * R; idx += 64) {
-        const uint32_t q = idx / R, srow = idx % R;
-        mA[q][srow] = static_cast<uint16_t>(srow < m ? 32u * minv(srow, q) : 0u);
+      for (uint32_t idx = lane; idx < m * (R / 4); idx += 64) {
+        const uint32_t q = idx / (R / 4), s0 = 4 * (idx % (R / 4));
+        uint32_t word = 0;
+        for (uint32_t b = 0; b < 4; ++b)
+          if (s0 + b < m) word |= minv(s0 + b, q) << (8 * b);
+        minvT[q][s0 / 4] = word;
       }
       __syncthreads();
       // Positions m..k-1: received sources ascending; D[s][j] = sum_q (M^-1)[s][q] * c(rep_q, j),
@@ -977,25 +962,29 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         for (uint32_t t2 = lane; t2 < cnt; t2 += 64) pin[pos_base + t2] = rl[t2];
         // reduced encoded sizes (detail/decoder.cc:402-404): szs[q] ^= c(q, j) (x) len_j over the
         // chunk's received sources; lanes split the sources, a wave XOR-reduction per repair.
-        for (uint32_t q = 0; q < m; ++q) {
-          const uint32_t R1 = rq1[q];
+        // Lane q owns repair q; the two length bytes multiply independently (galois_field.hh:
+        // 108-115), so one mul4 with the lane's table for c(q, j) codes a whole u16 length.
+        if (lane < m) {
+          const uint32_t R1 = rq1[lane];
           uint32_t e = 0;
-          for (uint32_t t2 = lane; t2 < cnt; t2 += 64)
-            e ^= msize(sl[t2], ((R1 + sidb + rl[t2] + 1u) * R1) % 255u + 1u);
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) e ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(e), o));
-          if (lane == 0) szs[q] ^= e;
+          for (uint32_t t2 = 0; t2 < cnt; ++t2) {
+            const uint32_t c = ((R1 + sidb + rl[t2] + 1u) * R1) % 255u + 1u;
+            const uint4 ab = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);
+            const uint32_t tf[5] = {ab.x, ab.y, ab.z, ab.w, d_perm.w[c][4]};
+            e ^= mul4(tf, sl[t2]);
+          }
+          szs[lane] ^= e;
         }
         if (!(a.ablate & 2u)) {
-          for (uint32_t p0 = 4 * lane; p0 < cnt; p0 += 256) {
+          for (uint32_t p0 = lane; p0 < cnt; p0 += 64) {
             uint8_t* dst = pc + static_cast<size_t>(pos_base + p0) * a.rp;
-            const uint32_t nb = min(4u, cnt - p0);
-            if (R == 8 || RM == 8) plan_dmac<8, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+            const uint32_t j = rl[p0];
+            if (R == 8 || RM == 8) plan_dcol<8, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
             else if constexpr (RM >= 16) {
-              if (R == 16 || RM == 16) plan_dmac<16, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+              if (R == 16 || RM == 16) plan_dcol<16, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
               else if constexpr (RM >= 32) {
-                if (R == 32 || RM == 32) plan_dmac<32, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
-                else if constexpr (RM >= 64) plan_dmac<64, RM>(m, p0, nb, sidb, rl, rq1, mA, dst, a.rp);
+                if (R == 32 || RM == 32) plan_dcol<32, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+                else if constexpr (RM >= 64) plan_dcol<64, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
               }
             }
           }
@@ -1006,7 +995,12 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
       // decoded size of missing source s = sum_q (M^-1)[s][q] (x) reduced size of repair q
       uint32_t sz = 0;
       if (lane < m)
-        for (uint32_t q = 0; q < m; ++q) sz ^= msize(szs[q], minv(lane, q));
+        for (uint32_t q = 0; q < m; ++q) {
+          const uint32_t c = minv(lane, q);
+          const uint4 ab = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);
+          const uint32_t tf[5] = {ab.x, ab.y, ab.z, ab.w, d_perm.w[c][4]};
+          sz ^= mul4(tf, szs[q]);
+        }
       if (lane < m) a.src_len[static_cast<size_t>(g) * k + miss[lane]] = static_cast<uint16_t>(sz);
     }
   }

@@ -90,6 +90,7 @@ ENCODE_CASES = [
     (3, 1, 1, 16, 16, True, "default"),               # minimum shape
     (2, 7, 3, 4096, 4112, True, "offset"),            # stride not a multiple of the wave span
     (5, 9, 12, 2080, 2080, True, "offset"),           # 2 KiB spans + a 1-lane tail; 8+4 row tiles
+    (6, 21, 20, 2048, 2048, False, "offset"),         # 3 row tiles: plane-sharing group, one idle wave
 ]
 
 
@@ -143,6 +144,7 @@ DECODE_CASES = [
     (10, 48, 40, 256, 256, "exact", 40, False),       # m = r = 40 (> one row tile)
     (9, 33, 12, 2080, 2080, "exact", 12, True),       # odd k (unaligned plan rows), 8+4 row tiles
     (30, 7, 5, 4096, 4096, "iid", 0.3, False),        # tiny k, mixed outcomes
+    (12, 45, 24, 2048, 2048, "mixed", 24, False),     # k % 4 != 0, 1-3 row tiles per generation
 ]
 
 

@@ -1,0 +1,64 @@
+"""VALU-op fraction of the MAC kernels from the SQ passes of tools/gpu_sq.sh -> profiles/pmc_valu.json.
+
+usage: python tools/pmc_valu.py <config> <sq/run_counter_collection.csv> <sq2/run_counter_collection.csv>
+
+Per launch (mean over dispatches; SQ counters are summed over the agent):
+  valu_lane_ops_per_byte_mac = 64 * SQ_INSTS_VALU / byte-MACs of the launch
+  valu_issue_frac            = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)
+                               (2 cycles per wave64 VALU op at full issue; GRBM_GUI_ACTIVE is
+                               summed over the 8 XCDs)
+  wave_cycles_split          = SQ_ACTIVE_INST_ANY / SQ_WAIT_ANY / SQ_WAIT_INST_ANY over SQ_WAVE_CYCLES
+bench.py copies the entry of its config into the bench line (roofline.valu_profile).
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
+           "decode_mac": (r"gf_mac_bj<\d+, true", r"gf_mac<\d, true")}
+CONFIGS = {"k128r32s4096": (128, 32, 4096, 4096, 32)}   # k, r, S, G, m
+
+
+def means(paths):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for p in paths:
+        for row in csv.DictReader(open(p)):
+            acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    cfg, *paths = sys.argv[1:]
+    k, r, S, G, m = CONFIGS[cfg]
+    table = means(paths)
+    out_p = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    out = json.load(open(out_p)) if os.path.exists(out_p) else {}
+    ent = {}
+    for key, names in KERNELS.items():
+        cs = next((v for n, v in table.items() if any(re.search(x, n) for x in names)), None)
+        if cs is None:
+            continue
+        macs = G * k * (r if key == "encode_mac" else m) * S
+        wc = cs["SQ_WAVE_CYCLES"]
+        ent[key] = {
+            "SQ_INSTS_VALU": cs["SQ_INSTS_VALU"],
+            "SQ_INSTS_SALU": cs["SQ_INSTS_SALU"],
+            "valu_lane_ops_per_byte_mac": round(64 * cs["SQ_INSTS_VALU"] / macs, 3),
+            "valu_issue_frac": round(cs["SQ_INSTS_VALU"] * 2 / (1024 * cs["GRBM_GUI_ACTIVE"] / 8), 3),
+            "wave_cycles_split": {"active": round(cs["SQ_ACTIVE_INST_ANY"] / wc, 3),
+                                  "wait_waitcnt": round(cs["SQ_WAIT_ANY"] / wc, 3),
+                                  "issue_stall": round(cs["SQ_WAIT_INST_ANY"] / wc, 3)},
+        }
+    out[cfg] = ent
+    out["note"] = ("SQ PMC passes (tools/gpu_sq.sh, tools/pmc_valu.py); VALU issue slots = 1024 SIMDs x "
+                   "(GRBM_GUI_ACTIVE/8) / 2 cycles per wave64 VALU op")
+    json.dump(out, open(out_p, "w"), indent=1)
+    print(json.dumps(ent, indent=1))
+
+
+if __name__ == "__main__":
+    main()

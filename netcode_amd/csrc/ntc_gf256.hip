@@ -467,7 +467,8 @@ __device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, ui
 }
 
 // ABL != 0: timing ablations of the encode kernel (NTC_GF256_BJ_ABLATE; results are wrong):
-// 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain.
+// 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain,
+// 16 every source uses source 0's jump offsets (scalar-cache-resident).
 template <int R, int RT, bool DEC, int ABL = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
@@ -549,7 +550,8 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     }
     const uint32_t i1 = clampk(i + 1);
 #pragma unroll
-    for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + static_cast<size_t>(i1) * jstep + 16 * h);
+    for (int h = 0; h < NJ; ++h)
+      on[h] = const_load<u32x16>(jrow + static_cast<size_t>((ABL & 16) ? 0u : i1) * jstep + 16 * h);
     if constexpr (!(ABL & 2)) {
       NTC_BJ_TABLES(Y)
     } else {
@@ -1148,6 +1150,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       case 4: fn = gf_mac_bj<8, false, 4>; break;
       case 8: fn = gf_mac_bj<8, false, 8>; break;
       case 11: fn = gf_mac_bj<8, false, 11>; break;
+      case 16: fn = gf_mac_bj<8, false, 16>; break;
 
       default: break;
     }

@@ -136,6 +136,54 @@ int  ntc_gf256_dense_decode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t n,
                                   const uint8_t* mat, const uint8_t* rep, uint8_t* out,
                                   uint8_t* ok, void* stream);
 
+/* ---- Wire format on the device (netcode/detail/packetizer.hh) ---------------------------------
+ * Packets live in fixed-size slots: packet p at pkts + p * pkt_stride (a multiple of 16), its
+ * length in pkt_len[p] -- the shape of a sendmmsg / recvmmsg batch.  Integers big-endian.
+ *
+ * ntc_gf256_write_repairs  <- packetizer::write_repair (packetizer.hh:90-122), called by
+ *   ntc::encoder::generate_repair (encoder.hh:321-333) once per repair: packet (g, j) =
+ *   [u8 1][u32 rid_base[g]+j][u16 rep_len[g]][symbol][ids][u16 rep_size[g][j]][u16 rep_len[g]]
+ *   [symbol] with ids = the generation's k source ids in write_ids' run-length form (:263-309).
+ *   rep/rep_size/rep_len as produced by ntc_gf256_encode_batch.  pkt_stride >=
+ *   ntc_gf256_repair_packet_bytes(k, stride).
+ * ntc_gf256_write_sources  <- packetizer::write_source (:165-183), called by ntc::encoder::
+ *   operator()(data) for systematic codes (encoder.hh:255-285): packet (g, i) =
+ *   [u8 2][u32 sid_base[g]+i][u16 src_len[g][i]][payload].  pkt_stride >= 7 + stride.
+ * ntc_gf256_read_packets   <- ntc::decoder::operator()(packet) (decoder.hh: get_packet_type
+ *   dispatch) + packetizer::read_source / read_repair (:125-158, 186-218): each packet is parsed
+ *   and its symbol scattered into the batch layout of ntc_gf256_decode_batch -- source id s to
+ *   slot (s - sid0) of src [G*k], repair id q to slot (q - rid0) of rep [G*r] (generation
+ *   g = slot / k or slot / r, i.e. sid_base[g] = sid0 + g*k, rid_base[g] = rid0 + g*r), zero-padded
+ *   to stride; src_len / src_mask / rep_size / rep_mask filled.  The call first zeroes the four
+ *   per-slot arrays (slots of packets not received keep their old bytes).  status[p] is one of
+ *   NTC_PKT_*; only NTC_PKT_SOURCE / NTC_PKT_REPAIR packets are stored.  A repair is stored only
+ *   when its id list is exactly its generation's k consecutive source ids (the batched decoder's
+ *   model).  Duplicate packets must carry identical bytes. */
+enum {
+  NTC_PKT_SOURCE = 0,          /* stored into src */
+  NTC_PKT_REPAIR = 1,          /* stored into rep */
+  NTC_PKT_ACK = 2,             /* an ack (type 0): not data, skipped */
+  NTC_PKT_BAD_TYPE = 3,        /* unknown type byte (reference: packet_type_error) */
+  NTC_PKT_OVERFLOW = 4,        /* truncated packet (reference: overflow_error) */
+  NTC_PKT_OUT_OF_BATCH = 5,    /* id outside [sid0, sid0 + G*k) / [rid0, rid0 + G*r) */
+  NTC_PKT_TOO_LARGE = 6,       /* symbol longer than stride */
+  NTC_PKT_NOT_GENERATION = 7   /* repair not over exactly its generation's k sources */
+};
+uint32_t ntc_gf256_repair_packet_bytes(uint32_t k, uint32_t stride);
+int  ntc_gf256_write_repairs(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
+                             uint32_t stride, const uint8_t* rep, const uint16_t* rep_size,
+                             const uint16_t* rep_len, const uint32_t* sid_base,
+                             const uint32_t* rid_base, uint8_t* out, uint32_t pkt_stride,
+                             uint32_t* pkt_len, void* stream);
+int  ntc_gf256_write_sources(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t stride,
+                             const uint8_t* src, const uint16_t* src_len, const uint32_t* sid_base,
+                             uint8_t* out, uint32_t pkt_stride, uint32_t* pkt_len, void* stream);
+int  ntc_gf256_read_packets(ntc_gf256_engine* eng, uint32_t npkts, const uint8_t* pkts,
+                            uint32_t pkt_stride, const uint32_t* pkt_len, uint32_t G, uint32_t k,
+                            uint32_t r, uint32_t stride, uint32_t sid0, uint32_t rid0,
+                            uint8_t* src, uint16_t* src_len, uint8_t* src_mask, uint8_t* rep,
+                            uint16_t* rep_size, uint8_t* rep_mask, uint8_t* status, void* stream);
+
 /* dst = c*src (add = 0) or dst ^= c*src (add = 1) over `len` bytes of device memory. */
 int  ntc_gf256_region_multiply(ntc_gf256_engine* eng, const uint8_t* src, uint8_t* dst,
                                size_t len, uint8_t c, int add, void* stream);

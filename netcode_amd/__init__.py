@@ -3,13 +3,14 @@ coding hot path).  The GF region multiply-accumulate, decode planning and Gauss-
 hand-written gfx950 HIP kernels in ``libntc_gf256.so`` (C ABI: include/netcode/gpu.h)."""
 from ._native import NativeError, load as load_native  # noqa: F401
 
-__all__ = ["NativeError", "load_native", "Engine", "GaloisField", "BatchEncoder", "BatchDecoder", "DenseCode"]
+__all__ = ["NativeError", "load_native", "Engine", "GaloisField", "BatchEncoder", "BatchDecoder", "DenseCode",
+           "Wire"]
 
 
 def __getattr__(name):
     # torch-dependent classes are imported lazily so the C-ABI checks work without torch.
     if name in ("Engine", "GaloisField", "BatchEncoder", "BatchDecoder", "status_to_numpy",
-                "STATUS_DTYPE", "EncodeResult", "DenseCode"):
+                "STATUS_DTYPE", "EncodeResult", "DenseCode", "Wire", "ReceivedBatch"):
         from . import engine
         return getattr(engine, name)
     raise AttributeError(name)

@@ -21,6 +21,8 @@ GPU_H_SYMBOLS = [
     "ntc_gf256_multiply_size", "ntc_gf256_multiply", "ntc_gf256_invert",
     "ntc_gf256_last_error", "ntc_gf256_build_info",
     "ntc_gf256_dense_invert_batch", "ntc_gf256_dense_encode_batch", "ntc_gf256_dense_decode_batch",
+    "ntc_gf256_repair_packet_bytes", "ntc_gf256_write_repairs", "ntc_gf256_write_sources",
+    "ntc_gf256_read_packets",
 ]
 
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "EUNSUPPORTED"}
@@ -78,6 +80,12 @@ def load(path: str | None = None):
     L.ntc_gf256_multiply.restype = u8
     L.ntc_gf256_invert.argtypes = [u8]
     L.ntc_gf256_invert.restype = u8
+    L.ntc_gf256_repair_packet_bytes.argtypes = [u32, u32]
+    L.ntc_gf256_repair_packet_bytes.restype = u32
+    L.ntc_gf256_write_repairs.argtypes = [V, u32, u32, u32, u32, P, P, P, P, P, P, u32, P, V]
+    L.ntc_gf256_write_sources.argtypes = [V, u32, u32, u32, P, P, P, P, u32, P, V]
+    L.ntc_gf256_read_packets.argtypes = [V, u32, P, u32, P, u32, u32, u32, u32, u32, u32,
+                                         P, P, P, P, P, P, P, V]
     L.ntc_gf256_last_error.restype = C.c_char_p
     L.ntc_gf256_build_info.restype = C.c_char_p
     for name in GPU_H_SYMBOLS:

@@ -234,6 +234,109 @@ class BatchDecoder:
         return status
 
 
+# Per-packet outcome of Wire.read_packets (NTC_PKT_* in include/netcode/gpu.h).
+PKT_SOURCE, PKT_REPAIR, PKT_ACK, PKT_BAD_TYPE, PKT_OVERFLOW, PKT_OUT_OF_BATCH, PKT_TOO_LARGE, \
+    PKT_NOT_GENERATION = range(8)
+
+
+@dataclass
+class ReceivedBatch:
+    """A batch layout filled from wire packets (the inputs of BatchDecoder)."""
+    src: torch.Tensor        # [G, k, stride] uint8
+    src_len: torch.Tensor    # [G, k] int16 (u16 bits)
+    src_mask: torch.Tensor   # [G, k] uint8
+    rep: torch.Tensor        # [G, r, stride] uint8
+    rep_size: torch.Tensor   # [G, r] int16 (u16 bits): encoded sizes
+    rep_mask: torch.Tensor   # [G, r] uint8
+    status: torch.Tensor     # [npkts] uint8, PKT_*
+
+
+class Wire:
+    """netcode's packetizer (netcode/detail/packetizer.hh) over whole batches on the device.
+
+    Packets live in fixed-size slots -- a [npkts, pkt_stride] uint8 tensor plus an [npkts] int32
+    length tensor, the shape of a sendmmsg / recvmmsg batch:
+
+    * :meth:`write_repairs` -- ``packetizer::write_repair`` (packetizer.hh:90-122) for every
+      repair of an :class:`EncodeResult`;
+    * :meth:`write_sources` -- ``packetizer::write_source`` (:165-183) for every source slot;
+    * :meth:`read_packets` -- ``decoder::operator()(packet)`` dispatch + ``read_source`` /
+      ``read_repair`` (:125-158, 186-218) into the :class:`BatchDecoder` layout.
+    """
+
+    def __init__(self, device: int | torch.device = 0):
+        self.engine = Engine.get(device)
+        self.device = self.engine.device
+
+    @staticmethod
+    def repair_packet_bytes(k: int, stride: int) -> int:
+        return int(_native.load().ntc_gf256_repair_packet_bytes(k, stride))
+
+    @staticmethod
+    def source_packet_bytes(stride: int) -> int:
+        return (7 + stride + 15) // 16 * 16
+
+    def _slots(self, n, pkt_stride):
+        return (torch.empty((n, pkt_stride), dtype=torch.uint8, device=self.device),
+                torch.empty((n,), dtype=torch.int32, device=self.device))
+
+    def write_repairs(self, enc: EncodeResult, k: int, sid_base: torch.Tensor | None = None,
+                      rid_base: torch.Tensor | None = None, pkt_stride: int | None = None):
+        G, r, stride = enc.repairs.shape
+        dev = self.device
+        for t, n in ((sid_base, "sid_base"), (rid_base, "rid_base")):
+            if t is not None:
+                _require(t, n, _U32, (G,), dev)
+        pkt_stride = pkt_stride or self.repair_packet_bytes(k, stride)
+        pkts, lens = self._slots(G * r, pkt_stride)
+        _native.check(_native.load().ntc_gf256_write_repairs(
+            self.engine.handle, G, k, r, stride, enc.repairs.data_ptr(),
+            enc.encoded_size.data_ptr(), enc.symbol_len.data_ptr(), _ptr(sid_base),
+            _ptr(rid_base), pkts.data_ptr(), pkt_stride, lens.data_ptr(), _stream(dev)),
+            "ntc_gf256_write_repairs")
+        return pkts, lens
+
+    def write_sources(self, src: torch.Tensor, src_len: torch.Tensor,
+                      sid_base: torch.Tensor | None = None, pkt_stride: int | None = None):
+        G, k, stride = src.shape
+        dev = self.device
+        _require(src, "src", _U8, (G, k, stride), dev)
+        _require(src_len, "src_len", _U16, (G, k), dev)
+        if sid_base is not None:
+            _require(sid_base, "sid_base", _U32, (G,), dev)
+        pkt_stride = pkt_stride or self.source_packet_bytes(stride)
+        pkts, lens = self._slots(G * k, pkt_stride)
+        _native.check(_native.load().ntc_gf256_write_sources(
+            self.engine.handle, G, k, stride, src.data_ptr(), src_len.data_ptr(), _ptr(sid_base),
+            pkts.data_ptr(), pkt_stride, lens.data_ptr(), _stream(dev)),
+            "ntc_gf256_write_sources")
+        return pkts, lens
+
+    def read_packets(self, pkts: torch.Tensor, pkt_len: torch.Tensor, G: int, k: int, r: int,
+                     stride: int, sid0: int = 0, rid0: int = 0,
+                     out: ReceivedBatch | None = None) -> ReceivedBatch:
+        n, pkt_stride = pkts.shape
+        dev = self.device
+        _require(pkts, "pkts", _U8, (n, pkt_stride), dev)
+        _require(pkt_len, "pkt_len", _U32, (n,), dev)
+        if out is None:
+            out = ReceivedBatch(
+                torch.empty((G, k, stride), dtype=torch.uint8, device=dev),
+                torch.empty((G, k), dtype=torch.int16, device=dev),
+                torch.empty((G, k), dtype=torch.uint8, device=dev),
+                torch.empty((G, r, stride), dtype=torch.uint8, device=dev),
+                torch.empty((G, r), dtype=torch.int16, device=dev),
+                torch.empty((G, r), dtype=torch.uint8, device=dev),
+                torch.empty((n,), dtype=torch.uint8, device=dev))
+        _native.check(_native.load().ntc_gf256_read_packets(
+            self.engine.handle, n, pkts.data_ptr(), pkt_stride, pkt_len.data_ptr(), G, k, r,
+            stride, sid0 & 0xFFFFFFFF, rid0 & 0xFFFFFFFF, out.src.data_ptr(),
+            out.src_len.data_ptr(), out.src_mask.data_ptr(), out.rep.data_ptr(),
+            out.rep_size.data_ptr(), out.rep_mask.data_ptr(), out.status.data_ptr(),
+            _stream(dev)), "ntc_gf256_read_packets")
+        return out
+
+
 def status_to_numpy(status: torch.Tensor) -> np.ndarray:
     """[G, 12] uint8 device tensor -> structured numpy array (STATUS_DTYPE)."""
     return status.cpu().numpy().view(STATUS_DTYPE).reshape(-1)

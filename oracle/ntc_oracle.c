@@ -937,6 +937,92 @@ static void read_ids(reader* r, u32set* out)
   }
 }
 
+/* ==================================================== wire format, packet by packet ====== */
+
+/* packetizer.hh:90-122 write_repair: type 1, id, symbol size, symbol, source ids, encoded size,
+   symbol size again, symbol again (all integers big-endian).  Returns the packet length. */
+size_t or_write_repair_packet(uint32_t rid, const uint8_t* sym, uint16_t symsz, const uint32_t* ids,
+                              size_t n, uint16_t esz, uint8_t* out)
+{
+  bytes b = {0};
+  b_u8(&b, 1);
+  b_u32(&b, rid);
+  b_u16(&b, symsz);
+  b_put(&b, sym, symsz);
+  write_ids(&b, ids, n);
+  b_u16(&b, esz);
+  b_u16(&b, symsz);
+  b_put(&b, sym, symsz);
+  memcpy(out, b.v, b.n);
+  const size_t len = b.n;
+  free(b.v);
+  return len;
+}
+
+/* packetizer.hh:165-183 write_source: type 2, id, size, payload. */
+size_t or_write_source_packet(uint32_t sid, const uint8_t* data, uint16_t len, uint8_t* out)
+{
+  bytes b = {0};
+  b_u8(&b, 2); b_u32(&b, sid); b_u16(&b, len); b_put(&b, data, len);
+  memcpy(out, b.v, b.n);
+  const size_t n = b.n;
+  free(b.v);
+  return n;
+}
+
+/* One received packet into a batch's generation layout: the device ingestion's specification
+   (ntc_gf256_read_packets, include/netcode/gpu.h).  Parsing follows packetizer.hh:125-158
+   (read_repair: the first symbol copy, ids, encoded size; overflow_error on truncation) and
+   :186-218 (read_source); get_packet_type (packet.hh) dispatches on byte 0.  Source id s lands in
+   generation (s - sid0) / k, slot (s - sid0) % k; repair id likewise with rid0 and r.  A repair is
+   stored only if its id list is exactly its generation's k consecutive source ids.  Slots are
+   zero-padded to `stride`.  Returns the status code (NTC_PKT_* in gpu.h). */
+int or_read_packet_into(const uint8_t* pkt, size_t len, uint32_t G, uint32_t k, uint32_t r,
+                        uint32_t stride, uint32_t sid0, uint32_t rid0, uint8_t* src,
+                        uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
+                        uint8_t* rep_mask)
+{
+  if (len == 0) return 4;
+  reader rd = {pkt, len, 0};
+  const uint8_t ty = r_u8(&rd);
+  if (ty == 0) return 2;
+  if (ty != 1 && ty != 2) return 3;
+  const uint32_t id = r_u32(&rd);
+  const uint16_t symsz = r_u16(&rd);
+  if (rd.err || rd.left < symsz) return 4;
+  const uint8_t* sym = rd.p;
+  rd.p += symsz; rd.left -= symsz;
+  if (ty == 2) {
+    const uint32_t d = id - sid0;
+    if ((uint64_t)d >= (uint64_t)G * k) return 5;
+    if (symsz > stride) return 6;
+    uint8_t* dst = src + (size_t)d * stride;
+    memcpy(dst, sym, symsz);
+    memset(dst + symsz, 0, stride - symsz);
+    src_len[d] = symsz;
+    src_mask[d] = 1;
+    return 0;
+  }
+  u32set ids;
+  read_ids(&rd, &ids);
+  const uint16_t esz = r_u16(&rd);
+  if (rd.err) { u32set_free(&ids); return 4; }
+  const uint32_t d = id - rid0;
+  if ((uint64_t)d >= (uint64_t)G * r) { u32set_free(&ids); return 5; }
+  if (symsz > stride) { u32set_free(&ids); return 6; }
+  const uint32_t g = d / r, sidb = sid0 + g * k;
+  int full = ids.n == k;
+  for (size_t i = 0; full && i < ids.n; ++i) full = ids.v[i] == sidb + (uint32_t)i;
+  u32set_free(&ids);
+  if (!full) return 7;
+  uint8_t* dst = rep + (size_t)d * stride;
+  memcpy(dst, sym, symsz);
+  memset(dst + symsz, 0, stride - symsz);
+  rep_size[d] = esz;
+  rep_mask[d] = 1;
+  return 1;
+}
+
 /* ======================================================== public encoder (encoder.hh) ====== */
 typedef struct { uint32_t id; uint16_t len; uint8_t* data; } esrc;
 

@@ -143,6 +143,16 @@ int  or_have_avx2(void);
 /* Route the oracle's own region ops through the AVX2 kernel (CPU baseline timing only). */
 void or_set_simd(int on);
 
+/* Wire format (packetizer.hh:90-122, 165-183) and one packet's ingestion into a batch layout
+ * (the specification of ntc_gf256_read_packets; status codes NTC_PKT_* of netcode/gpu.h). */
+size_t or_write_repair_packet(uint32_t rid, const uint8_t* sym, uint16_t symsz, const uint32_t* ids,
+                              size_t n, uint16_t esz, uint8_t* out);
+size_t or_write_source_packet(uint32_t sid, const uint8_t* data, uint16_t len, uint8_t* out);
+int or_read_packet_into(const uint8_t* pkt, size_t len, uint32_t G, uint32_t k, uint32_t r,
+                        uint32_t stride, uint32_t sid0, uint32_t rid0, uint8_t* src,
+                        uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
+                        uint8_t* rep_mask);
+
 #ifdef __cplusplus
 }
 #endif

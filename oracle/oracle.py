@@ -97,6 +97,12 @@ def lib():
         L.or_decoder_counter.argtypes = [P, C.c_int]
         L.or_have_avx2.restype = C.c_int
         L.or_set_simd.argtypes = [C.c_int]
+        L.or_write_repair_packet.restype = C.c_size_t
+        L.or_write_repair_packet.argtypes = [C.c_uint32, P, C.c_uint16, P, C.c_size_t, C.c_uint16, P]
+        L.or_write_source_packet.restype = C.c_size_t
+        L.or_write_source_packet.argtypes = [C.c_uint32, P, C.c_uint16, P]
+        L.or_read_packet_into.restype = C.c_int
+        L.or_read_packet_into.argtypes = [P, C.c_size_t] + [C.c_uint32] * 6 + [P] * 6
         _lib = L
     return _lib
 
@@ -193,6 +199,45 @@ def decode_batch(src, src_len, src_mask, rep, rep_size, rep_mask, sid_base=None,
                           _p(None if rid_base is None else np.ascontiguousarray(rid_base, np.uint32)),
                           _p(st), 0, int(threads))
     return s, sl, st
+
+
+# --------------------------------------------------------------------------- wire format
+def write_repair_packet(rid, sym, ids, esz) -> bytes:
+    """packetizer.hh:90-122: one repair packet (sym = the symbol bytes, ids ascending)."""
+    sym = np.ascontiguousarray(sym, np.uint8)
+    ids = np.ascontiguousarray(ids, np.uint32)
+    out = np.zeros(32 + 2 * sym.size + 3 * ids.size, np.uint8)
+    n = lib().or_write_repair_packet(rid & 0xFFFFFFFF, _p(sym), sym.size, _p(ids), ids.size, esz,
+                                     _p(out))
+    return out[:n].tobytes()
+
+
+def write_source_packet(sid, data) -> bytes:
+    """packetizer.hh:165-183: one source packet."""
+    data = np.ascontiguousarray(data, np.uint8)
+    out = np.zeros(16 + data.size, np.uint8)
+    n = lib().or_write_source_packet(sid & 0xFFFFFFFF, _p(data), data.size, _p(out))
+    return out[:n].tobytes()
+
+
+def read_packets(pkts, G, k, r, stride, sid0=0, rid0=0):
+    """Ingest wire packets (list of bytes) into a fresh batch layout; returns (src, src_len,
+    src_mask, rep, rep_size, rep_mask, status[npkts]) -- the specification of
+    ntc_gf256_read_packets."""
+    src = np.zeros((G, k, stride), np.uint8)
+    src_len = np.zeros((G, k), np.uint16)
+    src_mask = np.zeros((G, k), np.uint8)
+    rep = np.zeros((G, r, stride), np.uint8)
+    rep_size = np.zeros((G, r), np.uint16)
+    rep_mask = np.zeros((G, r), np.uint8)
+    st = np.zeros(len(pkts), np.uint8)
+    L = lib()
+    for i, p in enumerate(pkts):
+        b = np.frombuffer(p, np.uint8) if len(p) else np.zeros(1, np.uint8)
+        st[i] = L.or_read_packet_into(_p(b), len(p), G, k, r, stride, sid0 & 0xFFFFFFFF,
+                                      rid0 & 0xFFFFFFFF, _p(src), _p(src_len), _p(src_mask),
+                                      _p(rep), _p(rep_size), _p(rep_mask))
+    return src, src_len, src_mask, rep, rep_size, rep_mask, st
 
 
 def end_to_end(nb_packets: int):

@@ -758,6 +758,7 @@ __device__ __forceinline__ void plan_dcol(uint32_t m, uint32_t j, uint32_t sidb,
   uint32_t acc[R / 4];
 #pragma unroll
   for (int w = 0; w < R / 4; ++w) acc[w] = 0;
+#pragma unroll 4
   for (uint32_t q = 0; q < m; ++q) {
     const uint32_t R1 = rq1[q];
     const uint32_t c = ((R1 + S1) * R1) % 255u + 1u;   // galois_field.hh:143-158
@@ -897,6 +898,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
           uint32_t tf[5];
 #pragma unroll
           for (int e = 0; e < 5; ++e) tf[e] = d_perm.w[fa][e];
+#pragma unroll 4
           for (uint32_t w = 0; w < nw; ++w) A[lane][w] ^= mul4(tf, A[p][w]);
         }
         __syncthreads();
@@ -969,6 +971,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         if (lane < m) {
           const uint32_t R1 = rq1[lane];
           uint32_t e = 0;
+#pragma unroll 4
           for (uint32_t t2 = 0; t2 < cnt; ++t2) {
             const uint32_t c = ((R1 + sidb + rl[t2] + 1u) * R1) % 255u + 1u;
             const uint4 ab = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);
@@ -997,6 +1000,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
       // decoded size of missing source s = sum_q (M^-1)[s][q] (x) reduced size of repair q
       uint32_t sz = 0;
       if (lane < m)
+#pragma unroll 4
         for (uint32_t q = 0; q < m; ++q) {
           const uint32_t c = minv(lane, q);
           const uint4 ab = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);

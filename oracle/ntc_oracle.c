@@ -43,18 +43,113 @@ static inline void gf_init(void) { pthread_once(&g_once, gf_init_tables); }
 
 uint8_t or_gf_mul(uint8_t a, uint8_t b) { gf_init(); return g_mul[a][b]; }
 
-uint8_t or_gf_inv(uint8_t a)
+/* ------------------------------------------------ GF(2^w), w in {4, 8, 16, 32} (galois_field.hh) */
+/* galois_field.hh:35-44 gf_init_easy(&gf, w): gf-complete's default fields -- primitive
+ * polynomials 0x13 (w=4), 0x11D (w=8), 0x1100B (w=16), 0x400007 (+x^32, w=32).  gf-complete is not
+ * in /root/reference (no version pin); the polynomials are its published defaults, so for w != 8
+ * field bytes are "parity unpinned" against the reference and pinned by field invariants only.
+ * The field in use is per thread (the public encoder/decoder entry points select their own). */
+static __thread int g_w = 8;
+void or_set_field(int w) { g_w = w; }
+int or_field(void) { return g_w; }
+
+static uint64_t fw_poly(int w)
 {
-  /* galois_field.hh:133-139: divide.w32(1, c) */
-  gf_init();
-  return g_exp[(255 - g_log[a]) % 255];
+  return w == 4 ? 0x13u : w == 8 ? 0x11Du : w == 16 ? 0x1100Bu : 0x100400007ull;
 }
 
-/* galois_field.hh:143-158 (w = 8 branch): uint32 arithmetic with wraparound, then % 255 + 1. */
-uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id)
+/* carry-less product reduced by the field polynomial */
+uint32_t or_fw_mul(int w, uint32_t a, uint32_t b)
+{
+  if (a == 0 || b == 0) return 0;
+  if (w == 8) { gf_init(); return g_mul[a & 0xFF][b & 0xFF]; }
+  uint64_t r = 0;
+  for (int i = 0; i < w; ++i)
+    if ((b >> i) & 1u) r ^= (uint64_t)a << i;
+  const uint64_t p = fw_poly(w);
+  for (int i = 2 * w - 2; i >= w; --i)
+    if ((r >> i) & 1u) r ^= p << (i - w);
+  return (uint32_t)r;
+}
+
+/* galois_field.hh:133-139 divide.w32(1, c) = c^(2^w - 2) */
+uint32_t or_fw_inv(int w, uint32_t a)
+{
+  uint32_t res = 1, base = a;
+  uint64_t e = (w == 32 ? 0xFFFFFFFFull : ((1ull << w) - 1)) - 1;
+  while (e) {
+    if (e & 1) res = or_fw_mul(w, res, base);
+    base = or_fw_mul(w, base, base);
+    e >>= 1;
+  }
+  return res;
+}
+
+/* galois_field.hh:143-158: uint32 arithmetic with wraparound; % (2^w - 1) + 1 for w < 32, the raw
+ * product (0 -> 1) for w = 32. */
+uint32_t or_fw_coefficient(int w, uint32_t repair_id, uint32_t src_id)
 {
   const uint32_t res = ((repair_id + 1u) + (src_id + 1u)) * (repair_id + 1u);
-  return res % 255u + 1u;
+  if (w == 32) return res == 0 ? 1u : res;
+  return res % ((1u << w) - 1u) + 1u;
+}
+
+/* multiply_region.w32 semantics per w: w=4 every nibble, w=8 every byte, w=16 / w=32 every
+ * little-endian 16- / 32-bit word.  A trailing partial word reads missing bytes as zero and only
+ * the bytes inside `len` are written. */
+void or_fw_region(int w, const uint8_t* src, uint8_t* dst, size_t len, uint32_t c, int add)
+{
+  if (w == 4) {
+    for (size_t i = 0; i < len; ++i) {
+      const uint32_t lo = or_fw_mul(4, c, src[i] & 15u), hi = or_fw_mul(4, c, src[i] >> 4);
+      const uint8_t v = (uint8_t)((hi << 4) | lo);
+      dst[i] = add ? (uint8_t)(dst[i] ^ v) : v;
+    }
+    return;
+  }
+  if (w == 8) {
+    gf_init();
+    const uint8_t* row = g_mul[c & 0xFF];
+    for (size_t i = 0; i < len; ++i) dst[i] = add ? (uint8_t)(dst[i] ^ row[src[i]]) : row[src[i]];
+    return;
+  }
+  const size_t wb = (size_t)w / 8;
+  for (size_t i = 0; i < len; i += wb) {
+    uint32_t x = 0;
+    for (size_t b = 0; b < wb && i + b < len; ++b) x |= (uint32_t)src[i + b] << (8 * b);
+    const uint32_t v = or_fw_mul(w, c, x);
+    for (size_t b = 0; b < wb && i + b < len; ++b) {
+      const uint8_t o = (uint8_t)(v >> (8 * b));
+      dst[i + b] = add ? (uint8_t)(dst[i + b] ^ o) : o;
+    }
+  }
+}
+
+/* galois_field.hh:96-120: w <= 8 codes the u16 as a 2-byte region (native byte order); w = 16 a
+ * scalar product; w = 32 the GF(2^32) product truncated to 16 bits (:118). */
+uint16_t or_fw_multiply_size(int w, uint16_t size, uint32_t c)
+{
+  if (size == 0 || c == 0) return 0;
+  if (w <= 8) {
+    uint8_t in[2] = {(uint8_t)size, (uint8_t)(size >> 8)}, out[2];
+    or_fw_region(w, in, out, 2, c, 0);
+    return (uint16_t)(out[0] | (out[1] << 8));
+  }
+  return (uint16_t)or_fw_mul(w, size, c);
+}
+
+uint32_t or_gf_inv(uint32_t a)
+{
+  /* galois_field.hh:133-139: divide.w32(1, c) */
+  if (g_w != 8) return or_fw_inv(g_w, a);
+  gf_init();
+  return g_exp[(255 - g_log[a & 0xFF]) % 255];
+}
+
+/* galois_field.hh:143-158 (field of this thread; w = 8: % 255 + 1). */
+uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id)
+{
+  return or_fw_coefficient(g_w, repair_id, src_id);
 }
 
 static int g_simd = 0;   /* CPU-baseline mode: route region ops through the AVX2 kernel */
@@ -63,37 +158,35 @@ static void muladd_dispatch(const uint8_t* src, uint8_t* dst, size_t len, uint8_
 void or_set_simd(int on) { gf_init(); g_simd = on; }
 
 /* galois_field.hh:65-75: multiply_region.w32(..., add = 0) */
-void or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
+void or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint32_t c)
 {
   gf_init();
-  if (g_simd) { memset(dst, 0, len); muladd_dispatch(src, dst, len, c); return; }
-  const uint8_t* row = g_mul[c];
+  if (g_w != 8) { or_fw_region(g_w, src, dst, len, c, 0); return; }
+  if (g_simd) { memset(dst, 0, len); muladd_dispatch(src, dst, len, (uint8_t)c); return; }
+  const uint8_t* row = g_mul[c & 0xFF];
   for (size_t i = 0; i < len; ++i) dst[i] = row[src[i]];
 }
 
 /* galois_field.hh:83-92: multiply_region.w32(..., add = 1) */
-void or_region_muladd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
+void or_region_muladd(const uint8_t* src, uint8_t* dst, size_t len, uint32_t c)
 {
   gf_init();
-  if (g_simd) { muladd_dispatch(src, dst, len, c); return; }
-  const uint8_t* row = g_mul[c];
+  if (g_w != 8) { or_fw_region(g_w, src, dst, len, c, 1); return; }
+  if (g_simd) { muladd_dispatch(src, dst, len, (uint8_t)c); return; }
+  const uint8_t* row = g_mul[c & 0xFF];
   for (size_t i = 0; i < len; ++i) dst[i] ^= row[src[i]];
 }
 
-/* galois_field.hh:96-120 (w <= 8): the u16 is multiplied as a 2-byte region, byte by byte. */
+/* galois_field.hh:96-120 */
 uint16_t or_multiply_size(uint16_t size, uint32_t c)
 {
-  if (size == 0 || c == 0) return 0;
-  gf_init();
-  const uint8_t lo = g_mul[c & 0xFF][size & 0xFF];
-  const uint8_t hi = g_mul[c & 0xFF][size >> 8];
-  return (uint16_t)((hi << 8) | lo);
+  return or_fw_multiply_size(g_w, size, c);
 }
 
 static inline uint32_t gf_mul32(uint32_t x, uint32_t y)
 {
   /* galois_field.hh:123-130 */
-  return (x == 0 || y == 0) ? 0 : g_mul[x & 0xFF][y & 0xFF];
+  return or_fw_mul(g_w, x, y);
 }
 
 /* Dense codes (config 5 extension): plain region MACs over a caller-chosen matrix. */
@@ -151,7 +244,7 @@ long or_invert(uint32_t* mat, uint32_t* inv, size_t n)
     }
     const uint32_t tmp = mat[row_start + i];         /* :59-69 normalise */
     if (tmp != 1) {
-      const uint32_t inverse = or_gf_inv((uint8_t)tmp);
+      const uint32_t inverse = or_gf_inv(tmp);
       for (size_t j = 0; j < cols; ++j) {
         mat[row_start + j] = gf_mul32(mat[row_start + j], inverse);
         inv[row_start + j] = gf_mul32(inv[row_start + j], inverse);
@@ -503,14 +596,14 @@ static void remove_source_data_from_repair(const dsrc* s, drep* r)
 {
   const uint32_t c = or_coefficient(r->id, s->id);
   r->esz = (uint16_t)(or_multiply_size(s->len, c) ^ r->esz);
-  or_region_muladd(s->data, r->sym, s->len, (uint8_t)c);
+  or_region_muladd(s->data, r->sym, s->len, c);
 }
 
 /* detail/decoder.cc:156-178 */
 static dsrc create_source_from_repair(dec_core* d, const drep* r)
 {
   const uint32_t sid = r->ids.v[0];
-  const uint8_t inv = or_gf_inv((uint8_t)or_coefficient(r->id, sid));
+  const uint32_t inv = or_gf_inv(or_coefficient(r->id, sid));
   const uint16_t sz = or_multiply_size(r->esz, inv);
   dsrc s;
   s.id = sid; s.len = sz;
@@ -664,12 +757,12 @@ static int attempt_full_decoding(dec_core* d)
     uint32_t c = 0;
     for (; rr < n; ++rr) { c = inv[sc * n + rr]; if (c != 0) break; }
     size_t len = sz < d->rep[rr].symsz ? sz : d->rep[rr].symsz;
-    or_region_mul(d->rep[rr].sym, s.data, len, (uint8_t)c);
+    or_region_mul(d->rep[rr].sym, s.data, len, c);
     for (++rr; rr < n; ++rr) {
       c = inv[sc * n + rr];
       if (c != 0) {
         len = sz < d->rep[rr].symsz ? sz : d->rep[rr].symsz;
-        or_region_muladd(d->rep[rr].sym, s.data, len, (uint8_t)c);
+        or_region_muladd(d->rep[rr].sym, s.data, len, c);
       }
     }
     const uint32_t sid = s.id;
@@ -1027,6 +1120,7 @@ int or_read_packet_into(const uint8_t* pkt, size_t len, uint32_t G, uint32_t k, 
 typedef struct { uint32_t id; uint16_t len; uint8_t* data; } esrc;
 
 struct or_encoder {
+  int w;                                   /* Galois field size (galois_field.hh:35-44) */
   int systematic, adaptive;
   size_t rate, window_size;
   uint32_t cur_sid, cur_rid;
@@ -1040,6 +1134,7 @@ or_encoder* or_encoder_new(or_emit_fn emit, void* ctx)
 {
   gf_init();
   or_encoder* e = calloc(1, sizeof *e);
+  e->w = 8;
   e->systematic = 1; e->rate = 5; e->window_size = (size_t)-1;
   e->emit = emit; e->ctx = ctx;
   return e;
@@ -1060,7 +1155,7 @@ size_t or_encoder_nb_sent_sources(const or_encoder* e) { return e->nb_sources; }
 size_t or_encoder_nb_received_acks(const or_encoder* e) { return e->nb_acks; }
 
 /* encoder.hh:162-169, 321-333 + packetizer.hh:90-122 */
-void or_encoder_generate_repair(or_encoder* e)
+static void enc_generate_repair(or_encoder* e)
 {
   uint16_t symsz = 0;
   for (size_t i = 0; i < e->nwin; ++i) if (e->win[i].len > symsz) symsz = e->win[i].len;
@@ -1068,7 +1163,7 @@ void or_encoder_generate_repair(or_encoder* e)
   uint16_t esz = 0;
   uint32_t* ids = malloc((e->nwin + 1) * 4);
   for (size_t i = 0; i < e->nwin; ++i) {
-    const uint8_t c = (uint8_t)or_coefficient(e->cur_rid, e->win[i].id);
+    const uint32_t c = or_coefficient(e->cur_rid, e->win[i].id);
     if (i == 0) or_region_mul(e->win[i].data, sym, e->win[i].len, c);
     else or_region_muladd(e->win[i].data, sym, e->win[i].len, c);
     esz = (uint16_t)(or_multiply_size(e->win[i].len, c) ^ esz);
@@ -1092,7 +1187,7 @@ void or_encoder_generate_repair(or_encoder* e)
 }
 
 /* encoder.hh:255-285 */
-void or_encoder_add_data(or_encoder* e, const uint8_t* data, uint16_t len)
+static void enc_add_data(or_encoder* e, const uint8_t* data, uint16_t len)
 {
   if (e->nwin == e->window_size) {
     free(e->win[0].data);
@@ -1115,9 +1210,9 @@ void or_encoder_add_data(or_encoder* e, const uint8_t* data, uint16_t len)
     e->emit(e->ctx, b.v, b.n);
     free(b.v);
   } else {
-    or_encoder_generate_repair(e);
+    enc_generate_repair(e);
   }
-  if ((e->cur_sid + 1) % e->rate == 0) or_encoder_generate_repair(e);
+  if ((e->cur_sid + 1) % e->rate == 0) enc_generate_repair(e);
   e->cur_sid++;
 }
 
@@ -1159,6 +1254,7 @@ long or_encoder_add_packet(or_encoder* e, const uint8_t* pkt, size_t len)
 
 /* ======================================================== public decoder (decoder.hh) ====== */
 struct or_decoder {
+  int w;
   dec_core core;
   uint16_t ack_nb_packets;
   long ack_period_ms;
@@ -1210,6 +1306,7 @@ or_decoder* or_decoder_new(int in_order, or_emit_fn emit, void* ectx, or_deliver
 {
   gf_init();
   or_decoder* d = calloc(1, sizeof *d);
+  d->w = 8;
   core_init(&d->core, in_order, pub_handle_source, d);
   d->ack_nb_packets = 50;
   d->ack_period_ms = 100;
@@ -1237,7 +1334,7 @@ size_t or_decoder_counter(const or_decoder* d, int which)
 }
 
 /* decoder.hh:88-122 + packetizer.hh:125-218 */
-long or_decoder_add_packet(or_decoder* d, const uint8_t* pkt, size_t len)
+static long dec_add_packet(or_decoder* d, const uint8_t* pkt, size_t len)
 {
   if (len == 0) return -1;
   reader r = {pkt, len, 0};
@@ -1335,6 +1432,23 @@ static void e2e_deliver(void* ctx, uint32_t id, const uint8_t* data, size_t len)
   s->nb++;
   s->expected++;
 }
+
+/* Public entry points that do field arithmetic run in the object's field. */
+void or_encoder_generate_repair(or_encoder* e)
+{
+  const int old = g_w; g_w = e->w; enc_generate_repair(e); g_w = old;
+}
+void or_encoder_add_data(or_encoder* e, const uint8_t* data, uint16_t len)
+{
+  const int old = g_w; g_w = e->w; enc_add_data(e, data, len); g_w = old;
+}
+long or_decoder_add_packet(or_decoder* d, const uint8_t* pkt, size_t len)
+{
+  const int old = g_w; g_w = d->w; const long n = dec_add_packet(d, pkt, len); g_w = old;
+  return n;
+}
+void or_encoder_set_field(or_encoder* e, int w) { e->w = w; }
+void or_decoder_set_field(or_decoder* d, int w) { d->w = w; }
 
 int or_end_to_end(uint32_t nb_packets, uint64_t* out)
 {

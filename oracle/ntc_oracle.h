@@ -25,10 +25,11 @@ extern "C" {
 
 /* ---------------------------------------------------------------- GF(2^8) / 0x11D ---------- */
 uint8_t  or_gf_mul(uint8_t a, uint8_t b);
-uint8_t  or_gf_inv(uint8_t a);                     /* a != 0 */
-uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id);   /* galois_field.hh:143-158, w=8 */
-void     or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
-void     or_region_muladd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
+/* These run in the calling thread's field (GF(2^8) unless or_set_field chose another). */
+uint32_t or_gf_inv(uint32_t a);                   /* a != 0 */
+uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id);   /* galois_field.hh:143-158 */
+void     or_region_mul(const uint8_t* src, uint8_t* dst, size_t len, uint32_t c);
+void     or_region_muladd(const uint8_t* src, uint8_t* dst, size_t len, uint32_t c);
 uint16_t or_multiply_size(uint16_t size, uint32_t c);           /* galois_field.hh:96-120 */
 
 /* Jerasure Gauss-Jordan on a column-major square_matrix (invert_matrix.cc:9-128).
@@ -97,6 +98,7 @@ typedef void (*or_deliver_fn)(void* ctx, uint32_t id, const uint8_t* bytes, size
 
 or_encoder* or_encoder_new(or_emit_fn emit, void* ctx);
 void        or_encoder_free(or_encoder*);
+void        or_encoder_set_field(or_encoder*, int w);   /* galois_field_size, default 8 */
 void        or_encoder_set_rate(or_encoder*, size_t rate);
 void        or_encoder_set_window_size(or_encoder*, size_t sz);
 void        or_encoder_set_code_type(or_encoder*, int systematic);
@@ -112,6 +114,7 @@ size_t      or_encoder_nb_received_acks(const or_encoder*);
 
 or_decoder* or_decoder_new(int in_order, or_emit_fn emit, void* ectx, or_deliver_fn deliver,
                            void* dctx);
+void        or_decoder_set_field(or_decoder*, int w);
 void        or_decoder_free(or_decoder*);
 long        or_decoder_add_packet(or_decoder*, const uint8_t* pkt, size_t len); /* -1: err */
 void        or_decoder_generate_ack(or_decoder*);
@@ -142,6 +145,17 @@ void or_region_muladd_simd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t
 int  or_have_avx2(void);
 /* Route the oracle's own region ops through the AVX2 kernel (CPU baseline timing only). */
 void or_set_simd(int on);
+
+/* GF(2^w), w in {4, 8, 16, 32}: gf-complete's default polynomials 0x13 / 0x11D / 0x1100B /
+ * 0x400007 (galois_field.hh:35-44 gf_init_easy); region semantics per nibble / byte / LE u16 /
+ * LE u32 word; multiply_size per galois_field.hh:96-120 (w = 32 truncated). */
+void     or_set_field(int w);                      /* this thread's field for the calls above */
+int      or_field(void);
+uint32_t or_fw_mul(int w, uint32_t a, uint32_t b);
+uint32_t or_fw_inv(int w, uint32_t a);
+uint32_t or_fw_coefficient(int w, uint32_t repair_id, uint32_t src_id);
+void     or_fw_region(int w, const uint8_t* src, uint8_t* dst, size_t len, uint32_t c, int add);
+uint16_t or_fw_multiply_size(int w, uint16_t size, uint32_t c);
 
 /* Wire format (packetizer.hh:90-122, 165-183) and one packet's ingestion into a batch layout
  * (the specification of ntc_gf256_read_packets; status codes NTC_PKT_* of netcode/gpu.h). */

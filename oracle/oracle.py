@@ -49,14 +49,25 @@ def lib():
         u8p, u16p, u32p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint16), C.POINTER(C.c_uint32)
         L.or_gf_mul.restype = C.c_uint8
         L.or_gf_mul.argtypes = [C.c_uint8, C.c_uint8]
-        L.or_gf_inv.restype = C.c_uint8
-        L.or_gf_inv.argtypes = [C.c_uint8]
+        L.or_gf_inv.restype = C.c_uint32
+        L.or_gf_inv.argtypes = [C.c_uint32]
         L.or_coefficient.restype = C.c_uint32
         L.or_coefficient.argtypes = [C.c_uint32, C.c_uint32]
         L.or_multiply_size.restype = C.c_uint16
         L.or_multiply_size.argtypes = [C.c_uint16, C.c_uint32]
-        L.or_region_mul.argtypes = [P, P, C.c_size_t, C.c_uint8]
-        L.or_region_muladd.argtypes = [P, P, C.c_size_t, C.c_uint8]
+        L.or_region_mul.argtypes = [P, P, C.c_size_t, C.c_uint32]
+        L.or_region_muladd.argtypes = [P, P, C.c_size_t, C.c_uint32]
+        L.or_fw_mul.restype = C.c_uint32
+        L.or_fw_mul.argtypes = [C.c_int, C.c_uint32, C.c_uint32]
+        L.or_fw_inv.restype = C.c_uint32
+        L.or_fw_inv.argtypes = [C.c_int, C.c_uint32]
+        L.or_fw_coefficient.restype = C.c_uint32
+        L.or_fw_coefficient.argtypes = [C.c_int, C.c_uint32, C.c_uint32]
+        L.or_fw_region.argtypes = [C.c_int, P, P, C.c_size_t, C.c_uint32, C.c_int]
+        L.or_fw_multiply_size.restype = C.c_uint16
+        L.or_fw_multiply_size.argtypes = [C.c_int, C.c_uint16, C.c_uint32]
+        L.or_encoder_set_field.argtypes = [P, C.c_int]
+        L.or_decoder_set_field.argtypes = [P, C.c_int]
         L.or_region_muladd_simd.argtypes = [P, P, C.c_size_t, C.c_uint8]
         L.or_invert.restype = C.c_long
         L.or_invert.argtypes = [P, P, C.c_size_t]
@@ -201,6 +212,31 @@ def decode_batch(src, src_len, src_mask, rep, rep_size, rep_mask, sid_base=None,
     return s, sl, st
 
 
+# --------------------------------------------------------------------------- GF(2^w)
+def fw_mul(w: int, a: int, b: int) -> int:
+    return lib().or_fw_mul(w, a & 0xFFFFFFFF, b & 0xFFFFFFFF)
+
+
+def fw_inv(w: int, a: int) -> int:
+    return lib().or_fw_inv(w, a & 0xFFFFFFFF)
+
+
+def fw_coefficient(w: int, rid: int, sid: int) -> int:
+    return lib().or_fw_coefficient(w, rid & 0xFFFFFFFF, sid & 0xFFFFFFFF)
+
+
+def fw_multiply_size(w: int, size: int, c: int) -> int:
+    return lib().or_fw_multiply_size(w, size, c & 0xFFFFFFFF)
+
+
+def fw_region(w: int, src: np.ndarray, dst: np.ndarray, c: int, add: bool) -> np.ndarray:
+    """dst (copy) = c*src (+ dst) over len(src) bytes in GF(2^w)."""
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.ascontiguousarray(dst, np.uint8).copy()
+    lib().or_fw_region(w, _p(src), _p(out), src.size, c & 0xFFFFFFFF, int(add))
+    return out
+
+
 # --------------------------------------------------------------------------- wire format
 def write_repair_packet(rid, sym, ids, esz) -> bytes:
     """packetizer.hh:90-122: one repair packet (sym = the symbol bytes, ids ascending)."""
@@ -252,10 +288,11 @@ def end_to_end(nb_packets: int):
 class Encoder:
     """Packet-level restatement of ntc::encoder (encoder.hh); packets collected in .packets."""
 
-    def __init__(self):
+    def __init__(self, galois_field_size: int = 8):
         self.packets: list[bytes] = []
         self._cb = EMIT(lambda ctx, p, n: self.packets.append(C.string_at(p, n)))
         self.h = lib().or_encoder_new(self._cb, None)
+        lib().or_encoder_set_field(self.h, galois_field_size)
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -309,12 +346,13 @@ class Decoder:
                 "nb_received_repairs", "nb_received_sources", "nb_sent_acks",
                 "nb_useless_repairs", "nb_pending_repairs"]
 
-    def __init__(self, in_order: bool = True):
+    def __init__(self, in_order: bool = True, galois_field_size: int = 8):
         self.packets: list[bytes] = []
         self.data: list[tuple[int, bytes]] = []
         self._ecb = EMIT(lambda ctx, p, n: self.packets.append(C.string_at(p, n)))
         self._dcb = DELIVER(lambda ctx, i, p, n: self.data.append((i, C.string_at(p, n))))
         self.h = lib().or_decoder_new(int(in_order), self._ecb, None, self._dcb, None)
+        lib().or_decoder_set_field(self.h, galois_field_size)
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -12,7 +12,7 @@ extern "C" {
 typedef struct ntc_encoder_t ntc_encoder_t;
 typedef enum { ntc_systematic_yes, ntc_systematic_no } ntc_code_type;
 
-/* galois_field_size: 8 (this build implements GF(2^8)); NULL on OOM or unsupported size. */
+/* galois_field_size: 4, 8, 16 or 32; NULL on OOM, unsupported size or no MI355X engine. */
 ntc_encoder_t* ntc_new_encoder(uint8_t galois_field_size, ntc_packet_handler handler) NTC_C_NOEXCEPT;
 void   ntc_delete_encoder(ntc_encoder_t* enc) NTC_C_NOEXCEPT NTC_C_NONNULL;
 /* Consumes `data` (left empty: resize or delete it afterwards). */

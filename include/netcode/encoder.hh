@@ -28,7 +28,7 @@ public:
   encoder(encoder&&) = delete;
   encoder& operator=(encoder&&) = delete;
 
-  /// galois_field_size: 8 (this build implements GF(2^8); the reference also accepts 4/16/32).
+  /// galois_field_size: 4, 8, 16 or 32 (galois_field.hh:39).
   template <typename PacketHandler_>
   encoder(std::uint8_t galois_field_size, PacketHandler_&& packet_handler)
     : m_galois_field_size{galois_field_size}

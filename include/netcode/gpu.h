@@ -188,6 +188,31 @@ int  ntc_gf256_read_packets(ntc_gf256_engine* eng, uint32_t npkts, const uint8_t
 int  ntc_gf256_region_multiply(ntc_gf256_engine* eng, const uint8_t* src, uint8_t* dst,
                                size_t len, uint8_t c, int add, void* stream);
 
+/* ---- GF(2^w) for every field size netcode supports, w in {4, 8, 16, 32} --------------------
+ * galois_field.hh:35-44 gf_init_easy(&gf, w) -- gf-complete's default fields: primitive
+ * polynomials 0x13 (w=4), 0x11D (w=8), 0x1100B (w=16), x^32 + 0x400007 (w=32).  Regions follow
+ * multiply_region.w32: w=4 multiplies every nibble, w=8 every byte, w=16 / w=32 every
+ * little-endian 16- / 32-bit word (a partial last word reads missing bytes as zero and writes
+ * only bytes inside the region).  Coefficients are field elements (< 2^w).
+ *
+ * ntc_gf_combine_batch   <- the region MACs of detail/encoder.cc:15-64 and detail/decoder.cc
+ *   (:156-178, 393-408, 480-559) for any w: out[g][j] = sum_i coef[g][i][j] * in[g][i] over
+ *   `stride` bytes (stride a multiple of 16), coef [G][k][rows] u32.
+ * ntc_gf_region_multiply <- galois_field::multiply / multiply_add (galois_field.hh:65-92).
+ * ntc_gf_coefficient / ntc_gf_multiply / ntc_gf_invert / ntc_gf_multiply_size  <-
+ *   galois_field::coefficient (:143-158, w = 32: the raw uint32 product, 0 -> 1), multiply
+ *   (:123-130), invert (:133-139), multiply_size (:96-120; w = 32 truncates to 16 bits, :118).
+ *   Host-side, no device work; they return 0 for an unsupported w. */
+int  ntc_gf_combine_batch(ntc_gf256_engine* eng, uint32_t w, uint32_t G, uint32_t k, uint32_t rows,
+                          uint32_t stride, const uint8_t* in, const uint32_t* coef, uint8_t* out,
+                          void* stream);
+int  ntc_gf_region_multiply(ntc_gf256_engine* eng, uint32_t w, const uint8_t* src, uint8_t* dst,
+                            size_t len, uint32_t c, int add, void* stream);
+uint32_t ntc_gf_coefficient(uint32_t w, uint32_t repair_id, uint32_t src_id);
+uint32_t ntc_gf_multiply(uint32_t w, uint32_t x, uint32_t y);
+uint32_t ntc_gf_invert(uint32_t w, uint32_t x);
+uint16_t ntc_gf_multiply_size(uint32_t w, uint16_t size, uint32_t coeff);
+
 /* Host-side scalar helpers (no device work). */
 uint32_t ntc_gf256_coefficient(uint32_t repair_id, uint32_t src_id);
 uint16_t ntc_gf256_multiply_size(uint16_t size, uint32_t coeff);

@@ -10,7 +10,7 @@ __all__ = ["NativeError", "load_native", "Engine", "GaloisField", "BatchEncoder"
 def __getattr__(name):
     # torch-dependent classes are imported lazily so the C-ABI checks work without torch.
     if name in ("Engine", "GaloisField", "BatchEncoder", "BatchDecoder", "status_to_numpy",
-                "STATUS_DTYPE", "EncodeResult", "DenseCode", "Wire", "ReceivedBatch"):
+                "STATUS_DTYPE", "EncodeResult", "DenseCode", "Wire", "ReceivedBatch", "combine"):
         from . import engine
         return getattr(engine, name)
     raise AttributeError(name)

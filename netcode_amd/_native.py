@@ -23,6 +23,8 @@ GPU_H_SYMBOLS = [
     "ntc_gf256_dense_invert_batch", "ntc_gf256_dense_encode_batch", "ntc_gf256_dense_decode_batch",
     "ntc_gf256_repair_packet_bytes", "ntc_gf256_write_repairs", "ntc_gf256_write_sources",
     "ntc_gf256_read_packets",
+    "ntc_gf_combine_batch", "ntc_gf_region_multiply", "ntc_gf_coefficient", "ntc_gf_multiply",
+    "ntc_gf_invert", "ntc_gf_multiply_size",
 ]
 
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "EUNSUPPORTED"}
@@ -86,6 +88,15 @@ def load(path: str | None = None):
     L.ntc_gf256_write_sources.argtypes = [V, u32, u32, u32, P, P, P, P, u32, P, V]
     L.ntc_gf256_read_packets.argtypes = [V, u32, P, u32, P, u32, u32, u32, u32, u32, u32,
                                          P, P, P, P, P, P, P, V]
+    L.ntc_gf_combine_batch.argtypes = [V, u32, u32, u32, u32, u32, P, P, P, V]
+    L.ntc_gf_region_multiply.argtypes = [V, u32, P, P, C.c_size_t, u32, C.c_int, V]
+    for f in ("ntc_gf_coefficient", "ntc_gf_multiply"):
+        getattr(L, f).argtypes = [u32, u32, u32]
+        getattr(L, f).restype = u32
+    L.ntc_gf_invert.argtypes = [u32, u32]
+    L.ntc_gf_invert.restype = u32
+    L.ntc_gf_multiply_size.argtypes = [u32, u16, u32]
+    L.ntc_gf_multiply_size.restype = u16
     L.ntc_gf256_last_error.restype = C.c_char_p
     L.ntc_gf256_build_info.restype = C.c_char_p
     for name in GPU_H_SYMBOLS:

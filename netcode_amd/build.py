@@ -18,7 +18,8 @@ DEVFLAGS = ["-mllvm", "-structurizecfg-skip-uniform-regions"]
 
 TARGETS = {
     # GF(2^8) engine: kernels + batched C ABI (include/netcode/gpu.h)
-    "libntc_gf256.so": (["csrc/ntc_gf256.hip", "csrc/ntc_dense.hip", "csrc/ntc_wire.hip"], []),
+    "libntc_gf256.so": (["csrc/ntc_gf256.hip", "csrc/ntc_dense.hip", "csrc/ntc_wire.hip",
+                                          "csrc/ntc_gfw.hip"], []),
     # reference per-packet C ABI (include/netcode/c/*.h) over the engine
     "libntc.so": (["csrc/ntc_capi.cpp"], ["-L", "{here}", "-lntc_gf256", "-Wl,-rpath,$ORIGIN"]),
 }

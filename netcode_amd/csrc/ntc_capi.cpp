@@ -70,53 +70,44 @@ class Device {
   }
 
   // out[0..out_len) = sum_i c_i * in_i[0..len_i)  (inputs zero padded), one launch.
-  void combine(size_t n, const uint8_t* const* in, const uint16_t* lens, const uint8_t* coefs,
-               size_t out_len, uint8_t* out)
+  void combine(uint32_t w, size_t n, const uint8_t* const* in, const uint16_t* lens,
+               const uint32_t* coefs, size_t out_len, uint8_t* out)
+  {
+    uint8_t* outs[1] = {out};
+    combine_rows(w, n ? n : 0, in, lens, 1, coefs, out_len, outs);
+  }
+
+  // Several outputs from the same inputs: out_s = sum_i coef[i][s] * in_i (full decoding).
+  // GF(2^8): ntc_gf256_combine_batch (u8 coefficients, tile pitch); other fields:
+  // ntc_gf_combine_batch (u32 coefficients).
+  void combine_rows(uint32_t w, size_t n, const uint8_t* const* in, const uint16_t* lens,
+                    size_t rows, const uint32_t* coef /*[n][rows]*/, size_t out_len,
+                    uint8_t* const* out)
   {
     size_t mx = out_len;
     for (size_t i = 0; i < n; ++i) mx = std::max<size_t>(mx, lens[i]);
     const size_t stride = std::max<size_t>(16, (mx + 15) / 16 * 16);
-    const uint32_t pitch = ntc_gf256_coef_pitch(1);
-    const size_t nin = n ? n : 1;
-    grow(nin * stride, nin * pitch, stride);
+    const size_t nin = n ? n : 1;                  // an empty window combines a zero input
+    const uint32_t pitch = w == 8 ? ntc_gf256_coef_pitch(static_cast<uint32_t>(rows))
+                                  : static_cast<uint32_t>(4 * rows);
+    grow(nin * stride, nin * pitch, rows * stride);
     std::memset(h_in_, 0, nin * stride);
     std::memset(h_coef_, 0, nin * pitch);
     for (size_t i = 0; i < n; ++i) {
       std::memcpy(h_in_ + i * stride, in[i], lens[i]);
-      h_coef_[i * pitch] = coefs[i];
+      for (size_t s = 0; s < rows; ++s) {
+        if (w == 8) h_coef_[i * pitch + s] = static_cast<uint8_t>(coef[i * rows + s]);
+        else std::memcpy(h_coef_ + i * pitch + 4 * s, &coef[i * rows + s], 4);
+      }
     }
     check(hipMemcpyAsync(d_in_, h_in_, nin * stride, hipMemcpyHostToDevice, stream_), "H2D");
     check(hipMemcpyAsync(d_coef_, h_coef_, nin * pitch, hipMemcpyHostToDevice, stream_), "H2D");
-    const int rc = ntc_gf256_combine_batch(eng_, 1, static_cast<uint32_t>(nin), 1,
-                                           static_cast<uint32_t>(stride), d_in_, d_coef_, d_out_,
-                                           stream_);
-    if (rc) throw device_error(ntc_gf256_last_error());
-    check(hipMemcpyAsync(h_out_, d_out_, stride, hipMemcpyDeviceToHost, stream_), "D2H");
-    check(hipStreamSynchronize(stream_), "sync");
-    std::memcpy(out, h_out_, out_len);
-  }
-
-  // Several outputs from the same inputs: out_s = sum_i coef[i][s] * in_i (full decoding).
-  void combine_rows(size_t n, const uint8_t* const* in, const uint16_t* lens, size_t rows,
-                    const uint8_t* coef /*[n][rows]*/, size_t out_len, uint8_t* const* out)
-  {
-    size_t mx = out_len;
-    for (size_t i = 0; i < n; ++i) mx = std::max<size_t>(mx, lens[i]);
-    const size_t stride = std::max<size_t>(16, (mx + 15) / 16 * 16);
-    const uint32_t pitch = ntc_gf256_coef_pitch(static_cast<uint32_t>(rows));
-    grow(n * stride, n * pitch, rows * stride);
-    std::memset(h_in_, 0, n * stride);
-    std::memset(h_coef_, 0, n * pitch);
-    for (size_t i = 0; i < n; ++i) {
-      std::memcpy(h_in_ + i * stride, in[i], lens[i]);
-      for (size_t s = 0; s < rows; ++s) h_coef_[i * pitch + s] = coef[i * rows + s];
-    }
-    check(hipMemcpyAsync(d_in_, h_in_, n * stride, hipMemcpyHostToDevice, stream_), "H2D");
-    check(hipMemcpyAsync(d_coef_, h_coef_, n * pitch, hipMemcpyHostToDevice, stream_), "H2D");
-    const int rc = ntc_gf256_combine_batch(eng_, 1, static_cast<uint32_t>(n),
-                                           static_cast<uint32_t>(rows),
-                                           static_cast<uint32_t>(stride), d_in_, d_coef_, d_out_,
-                                           stream_);
+    const int rc = w == 8
+        ? ntc_gf256_combine_batch(eng_, 1, static_cast<uint32_t>(nin), static_cast<uint32_t>(rows),
+                                  static_cast<uint32_t>(stride), d_in_, d_coef_, d_out_, stream_)
+        : ntc_gf_combine_batch(eng_, w, 1, static_cast<uint32_t>(nin), static_cast<uint32_t>(rows),
+                               static_cast<uint32_t>(stride), d_in_,
+                               reinterpret_cast<const uint32_t*>(d_coef_), d_out_, stream_);
     if (rc) throw device_error(ntc_gf256_last_error());
     check(hipMemcpyAsync(h_out_, d_out_, rows * stride, hipMemcpyDeviceToHost, stream_), "D2H");
     check(hipStreamSynchronize(stream_), "sync");
@@ -178,9 +169,33 @@ class Device {
   uint64_t launches_ = 0;
 };
 
-inline uint8_t coef(uint32_t rid, uint32_t sid) { return static_cast<uint8_t>(ntc_gf256_coefficient(rid, sid)); }
-inline uint16_t msize(uint16_t s, uint32_t c) { return ntc_gf256_multiply_size(s, c); }
-inline uint32_t gmul(uint32_t a, uint32_t b) { return ntc_gf256_multiply(static_cast<uint8_t>(a), static_cast<uint8_t>(b)); }
+// galois_field (galois_field.hh:18-167) for the field size an encoder / decoder was built with:
+// GF(2^8) through the engine's tables, w in {4, 16, 32} through ntc_gf_* (gpu.h).
+struct Field {
+  uint32_t w;
+  explicit Field(uint32_t w_) : w(w_)
+  {
+    if (w != 4 && w != 8 && w != 16 && w != 32)
+      throw std::invalid_argument("galois field size must be 4, 8, 16 or 32");
+  }
+  uint32_t coef(uint32_t rid, uint32_t sid) const
+  {
+    return w == 8 ? ntc_gf256_coefficient(rid, sid) : ntc_gf_coefficient(w, rid, sid);
+  }
+  uint16_t msize(uint16_t s, uint32_t c) const
+  {
+    return w == 8 ? ntc_gf256_multiply_size(s, c) : ntc_gf_multiply_size(w, s, c);
+  }
+  uint32_t mul(uint32_t a, uint32_t b) const
+  {
+    return w == 8 ? ntc_gf256_multiply(static_cast<uint8_t>(a), static_cast<uint8_t>(b))
+                  : ntc_gf_multiply(w, a, b);
+  }
+  uint32_t inv(uint32_t a) const
+  {
+    return w == 8 ? ntc_gf256_invert(static_cast<uint8_t>(a)) : ntc_gf_invert(w, a);
+  }
+};
 
 // --------------------------------------------------------------------------- wire format ----
 // Big-endian fields; id lists RLE-coded on 16-bit deltas (detail/packetizer.hh:263-352).
@@ -263,11 +278,7 @@ namespace ntcx {
 // ============================================================================== encoder ====
 class Encoder {
  public:
-  Encoder(uint8_t w, ntc_packet_handler h) : out_{h}
-  {
-    if (w != 8) throw std::invalid_argument("this build implements GF(2^8) only");
-    Device::get();
-  }
+  Encoder(uint8_t w, ntc_packet_handler h) : f_(w), out_{h} { Device::get(); }
 
   // encoder.hh:255-285
   void add_data(bytes&& d)
@@ -296,20 +307,20 @@ class Encoder {
     if (window_.empty()) throw std::runtime_error("generate_repair on an empty window");
     std::vector<const uint8_t*> in;
     std::vector<uint16_t> lens;
-    std::vector<uint8_t> cs;
+    std::vector<uint32_t> cs;
     std::vector<uint32_t> ids;
     uint16_t symsz = 0, esz = 0;
     for (const Src& s : window_) {
-      const uint8_t c = coef(cur_rid_, s.id);
+      const uint32_t c = f_.coef(cur_rid_, s.id);
       in.push_back(s.sym.data());
       lens.push_back(static_cast<uint16_t>(s.sym.size()));
       cs.push_back(c);
       ids.push_back(s.id);
       symsz = std::max<uint16_t>(symsz, static_cast<uint16_t>(s.sym.size()));
-      esz = static_cast<uint16_t>(msize(static_cast<uint16_t>(s.sym.size()), c) ^ esz);
+      esz = static_cast<uint16_t>(f_.msize(static_cast<uint16_t>(s.sym.size()), c) ^ esz);
     }
     bytes sym(symsz);
-    Device::get().combine(in.size(), in.data(), lens.data(), cs.data(), symsz, sym.data());
+    Device::get().combine(f_.w, in.size(), in.data(), lens.data(), cs.data(), symsz, sym.data());
     const uint32_t rid = cur_rid_++;
     ++nb_repairs_;
     ++nb_sent_packets_;
@@ -373,6 +384,7 @@ class Encoder {
     uint32_t id;
     bytes sym;
   };
+  Field f_;
   Writer out_;
   std::list<Src> window_;
   size_t rate_ = 5;
@@ -389,9 +401,8 @@ class Encoder {
 class Decoder {
  public:
   Decoder(uint8_t w, bool in_order, ntc_packet_handler ph, ntc_data_handler dh)
-      : in_order_(in_order), out_{ph}, dh_(dh), last_ack_(std::chrono::steady_clock::now())
+      : f_(w), in_order_(in_order), out_{ph}, dh_(dh), last_ack_(std::chrono::steady_clock::now())
   {
-    if (w != 8) throw std::invalid_argument("this build implements GF(2^8) only");
     Device::get();
   }
 
@@ -512,27 +523,27 @@ class Decoder {
     if (known.empty()) return;
     std::vector<const uint8_t*> in{r.sym.data()};
     std::vector<uint16_t> lens{r.symsz};
-    std::vector<uint8_t> cs{1};
+    std::vector<uint32_t> cs{1};
     for (const Src* s : known) {
-      const uint8_t c = coef(r.id, s->id);
-      r.esz = static_cast<uint16_t>(msize(s->size, c) ^ r.esz);
+      const uint32_t c = f_.coef(r.id, s->id);
+      r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
       in.push_back(s->sym.data());
       lens.push_back(std::min<uint16_t>(s->size, r.symsz));
       cs.push_back(c);
     }
-    Device::get().combine(in.size(), in.data(), lens.data(), cs.data(), r.symsz, r.sym.data());
+    Device::get().combine(f_.w, in.size(), in.data(), lens.data(), cs.data(), r.symsz, r.sym.data());
   }
 
   // detail/decoder.cc:156-178
   Src create_source_from_repair(const Rep& r)
   {
     const uint32_t sid = r.ids.front();
-    const uint8_t inv = ntc_gf256_invert(coef(r.id, sid));
-    const uint16_t sz = msize(r.esz, inv);
+    const uint32_t inv = f_.inv(f_.coef(r.id, sid));
+    const uint16_t sz = f_.msize(r.esz, inv);
     Src s{sid, bytes(std::max<size_t>(sz, 1), 0), sz};
     const uint8_t* in = r.sym.data();
     const uint16_t len = std::min(sz, r.symsz);
-    Device::get().combine(1, &in, &len, &inv, sz, s.sym.data());
+    Device::get().combine(f_.w, 1, &in, &len, &inv, sz, s.sym.data());
     nb_decoded_ += 1;
     return s;
   }
@@ -655,7 +666,7 @@ class Decoder {
   // detail/invert_matrix.cc:9-128 semantics: returns false on a singular matrix (the reference
   // then reports index rows-1); inv is the unique inverse otherwise.  M is [n][n] row-major,
   // row = repair, column = missing source (the reference's storage rows).
-  static bool invert(std::vector<uint32_t> M, size_t n, std::vector<uint32_t>& inv)
+  bool invert(std::vector<uint32_t> M, size_t n, std::vector<uint32_t>& inv) const
   {
     inv.assign(n * n, 0);
     for (size_t i = 0; i < n; ++i) inv[i * n + i] = 1;
@@ -665,12 +676,12 @@ class Decoder {
       if (p == n) return false;
       if (p != i)
         for (size_t k = 0; k < n; ++k) { std::swap(M[i * n + k], M[p * n + k]); std::swap(inv[i * n + k], inv[p * n + k]); }
-      const uint32_t piv = ntc_gf256_invert(static_cast<uint8_t>(M[i * n + i]));
-      for (size_t k = 0; k < n; ++k) { M[i * n + k] = gmul(M[i * n + k], piv); inv[i * n + k] = gmul(inv[i * n + k], piv); }
+      const uint32_t piv = f_.inv(M[i * n + i]);
+      for (size_t k = 0; k < n; ++k) { M[i * n + k] = f_.mul(M[i * n + k], piv); inv[i * n + k] = f_.mul(inv[i * n + k], piv); }
       for (size_t j = 0; j < n; ++j) {
         if (j == i || M[j * n + i] == 0) continue;
         const uint32_t f = M[j * n + i];
-        for (size_t k = 0; k < n; ++k) { M[j * n + k] ^= gmul(f, M[i * n + k]); inv[j * n + k] ^= gmul(f, inv[i * n + k]); }
+        for (size_t k = 0; k < n; ++k) { M[j * n + k] ^= f_.mul(f, M[i * n + k]); inv[j * n + k] ^= f_.mul(f, inv[i * n + k]); }
       }
     }
     return true;
@@ -690,7 +701,7 @@ class Decoder {
     for (size_t q = 0; q < n; ++q)
       for (size_t s = 0; s < n; ++s)
         if (std::binary_search(reps[q]->ids.begin(), reps[q]->ids.end(), mids[s]))
-          M[q * n + s] = coef(reps[q]->id, mids[s]);
+          M[q * n + s] = f_.coef(reps[q]->id, mids[s]);
     if (!invert(M, n, inv)) {                      // :448-468 drop the repair at index rows-1
       ++nb_failed_;
       auto last = std::prev(repairs_.end());
@@ -703,7 +714,7 @@ class Decoder {
     for (size_t s = 0; s < n; ++s)
       for (size_t q = 0; q < n; ++q) {
         const uint32_t c = inv[s * n + q];
-        if (c) sizes[s] = static_cast<uint16_t>(msize(reps[q]->esz, c) ^ sizes[s]);
+        if (c) sizes[s] = static_cast<uint16_t>(f_.msize(reps[q]->esz, c) ^ sizes[s]);
       }
     std::vector<Src> dec(n);
     std::vector<uint8_t*> outs(n);
@@ -715,17 +726,17 @@ class Decoder {
     }
     std::vector<const uint8_t*> in(n);
     std::vector<uint16_t> lens(n);
-    std::vector<uint8_t> cf(n * n);
+    std::vector<uint32_t> cf(n * n);
     for (size_t q = 0; q < n; ++q) {
       in[q] = reps[q]->sym.data();
       lens[q] = reps[q]->symsz;
-      for (size_t s = 0; s < n; ++s) cf[q * n + s] = static_cast<uint8_t>(inv[s * n + q]);
+      for (size_t s = 0; s < n; ++s) cf[q * n + s] = inv[s * n + q];
     }
     // one launch for all missing sources; bytes past each decoded size are dropped below
     std::vector<bytes> full(n, bytes(std::max<size_t>(mx, 1), 0));
     std::vector<uint8_t*> fo(n);
     for (size_t s = 0; s < n; ++s) fo[s] = full[s].data();
-    Device::get().combine_rows(n, in.data(), lens.data(), n, cf.data(), mx, fo.data());
+    Device::get().combine_rows(f_.w, n, in.data(), lens.data(), n, cf.data(), mx, fo.data());
     for (size_t s = 0; s < n; ++s) {
       // the reference reads min(src_sz, repair.symbol_size()) bytes of each repair (:523, :531)
       std::memcpy(dec[s].sym.data(), full[s].data(), sizes[s]);
@@ -746,6 +757,7 @@ class Decoder {
     missing_.clear();
   }
 
+  Field f_;
   bool in_order_;
   Writer out_;
   ntc_data_handler dh_;

@@ -1,0 +1,207 @@
+// ntc_gfw.hip -- GF(2^w) for every field size netcode supports, w in {4, 8, 16, 32}
+// (galois_field.hh:35-44 gf_init_easy(&gf, w)).
+//
+// The fields are gf-complete's defaults: primitive polynomials 0x13 (w=4), 0x11D (w=8), 0x1100B
+// (w=16), x^32 + 0x400007 (w=32).  Region semantics of multiply_region.w32: w=4 multiplies every
+// nibble, w=8 every byte, w=16 / w=32 every little-endian 16- / 32-bit word of the region.
+//
+// Device work is a shift-and-add multiply on packed elements: a dword holds 8 / 4 / 2 / 1
+// elements, xtime (multiply by alpha) is a masked shift plus a reduction constant for all of them
+// at once, and the wave-uniform coefficient's bits select which powers are accumulated -- at most
+// w xtime steps per dword and input, no tables.  This serves the per-packet C ABI (libntc.so) for
+// w != 8 and the batched combine for any w; the GF(2^8) batch path keeps its dedicated kernels
+// (ntc_gf256.hip).  Host-side scalar arithmetic (coefficient, multiply, invert, multiply_size) is
+// the carry-less product reduced by the same polynomials.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "engine.hh"
+#include "netcode/gpu.h"
+
+namespace ntcgpu {
+namespace {
+
+template <int W> struct Packed;
+template <> struct Packed<4> {
+  static constexpr uint32_t keep = 0xEEEEEEEEu, top = 0x11111111u, red = 0x3u, shift = 3;
+};
+template <> struct Packed<8> {
+  static constexpr uint32_t keep = 0xFEFEFEFEu, top = 0x01010101u, red = 0x1Du, shift = 7;
+};
+template <> struct Packed<16> {
+  static constexpr uint32_t keep = 0xFFFEFFFEu, top = 0x00010001u, red = 0x100Bu, shift = 15;
+};
+
+// alpha * x for every element packed in x
+template <int W>
+__device__ __forceinline__ uint32_t xtime(uint32_t y)
+{
+  if constexpr (W == 32) {
+    return (y << 1) ^ ((0u - (y >> 31)) & 0x00400007u);
+  } else {
+    return ((y << 1) & Packed<W>::keep) ^ (((y >> Packed<W>::shift) & Packed<W>::top) * Packed<W>::red);
+  }
+}
+
+// c * x for every element packed in x (the loop ends after c's top bit; uniform when c is).
+template <int W>
+__device__ __forceinline__ uint32_t mulw(uint32_t c, uint32_t x)
+{
+  uint32_t r = 0, y = x;
+  for (int t = 0; t < W; ++t) {
+    const uint32_t ct = c >> t;
+    if (ct == 0) break;
+    if (ct & 1u) r ^= y;
+    y = xtime<W>(y);
+  }
+  return r;
+}
+
+struct CombineArgs {
+  uint32_t G, k, rows, stride;
+  const uint8_t* in;       // [G][k][stride]
+  const uint32_t* coef;    // [G][k][rows]
+  uint8_t* out;            // [G][rows][stride]
+};
+
+// One thread per 16-byte column chunk of one output row.
+template <int W>
+__global__ __launch_bounds__(256) void gfw_combine(CombineArgs a)
+{
+  const uint32_t chunks = a.stride / 16u;
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t per_g = static_cast<uint64_t>(a.rows) * chunks;
+  if (t >= per_g * a.G) return;
+  const uint32_t g = static_cast<uint32_t>(t / per_g);
+  const uint32_t rem = static_cast<uint32_t>(t % per_g);
+  const uint32_t j = rem / chunks, col = 16u * (rem % chunks);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  const uint8_t* in = a.in + static_cast<size_t>(g) * a.k * a.stride + col;
+  const uint32_t* cf = a.coef + static_cast<size_t>(g) * a.k * a.rows + j;
+  for (uint32_t i = 0; i < a.k; ++i) {
+    const uint32_t c = cf[static_cast<size_t>(i) * a.rows];   // per lane: a wave spans rows
+    if (c == 0) continue;
+    const uint4 x = *reinterpret_cast<const uint4*>(in + static_cast<size_t>(i) * a.stride);
+    acc.x ^= mulw<W>(c, x.x);
+    acc.y ^= mulw<W>(c, x.y);
+    acc.z ^= mulw<W>(c, x.z);
+    acc.w ^= mulw<W>(c, x.w);
+  }
+  *reinterpret_cast<uint4*>(a.out + (static_cast<size_t>(g) * a.rows + j) * a.stride + col) = acc;
+}
+
+// dst[0..len) = c * src (+ dst); word boundaries relative to the region start; a partial last word
+// reads missing bytes as zero and writes only bytes inside len.
+template <int W>
+__global__ __launch_bounds__(256) void gfw_region(const uint8_t* __restrict__ src, uint8_t* dst,
+                                                  uint64_t len, uint32_t c, int add)
+{
+  const uint64_t d = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t b0 = 4 * d;
+  if (b0 >= len) return;
+  const uint32_t nb = static_cast<uint32_t>(len - b0 < 4 ? len - b0 : 4);
+  uint32_t x = 0;
+  for (uint32_t b = 0; b < nb; ++b) x |= static_cast<uint32_t>(src[b0 + b]) << (8 * b);
+  const uint32_t y = mulw<W>(c, x);
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint8_t o = static_cast<uint8_t>(y >> (8 * b));
+    dst[b0 + b] = add ? static_cast<uint8_t>(dst[b0 + b] ^ o) : o;
+  }
+}
+
+bool valid_w(uint32_t w) { return w == 4 || w == 8 || w == 16 || w == 32; }
+
+uint64_t host_poly(uint32_t w)
+{
+  return w == 4 ? 0x13u : w == 8 ? 0x11Du : w == 16 ? 0x1100Bu : 0x100400007ull;
+}
+
+}  // namespace
+}  // namespace ntcgpu
+
+using namespace ntcgpu;
+
+extern "C" {
+
+uint32_t ntc_gf_multiply(uint32_t w, uint32_t a, uint32_t b)
+{
+  if (!valid_w(w) || a == 0 || b == 0) return 0;
+  uint64_t r = 0;
+  for (uint32_t i = 0; i < w; ++i)
+    if ((b >> i) & 1u) r ^= static_cast<uint64_t>(a) << i;
+  const uint64_t p = host_poly(w);
+  for (int i = 2 * static_cast<int>(w) - 2; i >= static_cast<int>(w); --i)
+    if ((r >> i) & 1u) r ^= p << (i - static_cast<int>(w));
+  return static_cast<uint32_t>(r);
+}
+
+uint32_t ntc_gf_invert(uint32_t w, uint32_t a)
+{
+  if (!valid_w(w) || a == 0) return 0;
+  uint32_t res = 1, base = a;
+  uint64_t e = (w == 32 ? 0xFFFFFFFFull : ((1ull << w) - 1)) - 1;   // a^(2^w - 2)
+  while (e) {
+    if (e & 1) res = ntc_gf_multiply(w, res, base);
+    base = ntc_gf_multiply(w, base, base);
+    e >>= 1;
+  }
+  return res;
+}
+
+uint32_t ntc_gf_coefficient(uint32_t w, uint32_t repair_id, uint32_t src_id)
+{
+  if (!valid_w(w)) return 0;
+  const uint32_t res = ((repair_id + 1u) + (src_id + 1u)) * (repair_id + 1u);
+  if (w == 32) return res == 0 ? 1u : res;
+  return res % ((1u << w) - 1u) + 1u;
+}
+
+uint16_t ntc_gf_multiply_size(uint32_t w, uint16_t size, uint32_t c)
+{
+  if (!valid_w(w) || size == 0 || c == 0) return 0;
+  if (w == 4) {          // the u16's four nibbles, each multiplied by c
+    uint32_t r = 0;
+    for (int n = 0; n < 4; ++n) r |= ntc_gf_multiply(4, c, (size >> (4 * n)) & 15u) << (4 * n);
+    return static_cast<uint16_t>(r);
+  }
+  if (w == 8) return static_cast<uint16_t>(ntc_gf_multiply(8, c, size & 0xFFu) |
+                                           (ntc_gf_multiply(8, c, size >> 8) << 8));
+  return static_cast<uint16_t>(ntc_gf_multiply(w, size, c));   // w = 32: truncated
+}
+
+int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k, uint32_t rows,
+                         uint32_t stride, const uint8_t* in, const uint32_t* coef, uint8_t* out,
+                         void* stream)
+{
+  if (!e || !in || !coef || !out) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (!valid_w(w)) return fail(NTC_GPU_EINVAL, "w must be 4, 8, 16 or 32");
+  if (G == 0 || k == 0 || rows == 0) return fail(NTC_GPU_EINVAL, "G, k and rows must be > 0");
+  if (stride == 0 || stride % 16 != 0) return fail(NTC_GPU_EINVAL, "stride must be a non-zero multiple of 16");
+  const uint64_t threads = static_cast<uint64_t>(G) * rows * (stride / 16u);
+  const uint64_t blocks = (threads + 255) / 256;
+  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
+  (void)hipSetDevice(e->device);
+  CombineArgs a{G, k, rows, stride, in, coef, out};
+  auto* fn = w == 4 ? gfw_combine<4> : w == 8 ? gfw_combine<8> : w == 16 ? gfw_combine<16> : gfw_combine<32>;
+  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a);
+  return hip_check(hipGetLastError(), "gfw_combine launch");
+}
+
+int ntc_gf_region_multiply(ntc_gf256_engine* e, uint32_t w, const uint8_t* src, uint8_t* dst,
+                           size_t len, uint32_t c, int add, void* stream)
+{
+  if (!e || (len && (!src || !dst))) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (!valid_w(w)) return fail(NTC_GPU_EINVAL, "w must be 4, 8, 16 or 32");
+  if (len == 0) return NTC_GPU_OK;
+  const uint64_t blocks = (len / 4 + 1 + 255) / 256;
+  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "region too large for one launch");
+  (void)hipSetDevice(e->device);
+  auto* fn = w == 4 ? gfw_region<4> : w == 8 ? gfw_region<8> : w == 16 ? gfw_region<16> : gfw_region<32>;
+  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), src, dst, static_cast<uint64_t>(len), c, add);
+  return hip_check(hipGetLastError(), "gfw_region launch");
+}
+
+}  // extern "C"

@@ -4,7 +4,8 @@ Python surface (device tensors in, device tensors out; the GF work runs in libnt
 
 * :class:`GaloisField`  -- ``ntc::detail::galois_field`` (netcode/detail/galois_field.hh:18-167):
   ``coefficient``, ``multiply`` / ``multiply_add`` (device regions), ``multiply_size``,
-  scalar ``multiply`` / ``invert``.  w = 8 only in this build.
+  scalar ``multiply`` / ``invert`` for w in {4, 8, 16, 32}; :func:`combine` batched GF(2^w)
+  combinations.
 * :class:`BatchEncoder` -- ``ntc::detail::encoder`` (netcode/detail/encoder.cc:15-64) applied to
   G independent generations of k sources -> r repairs each.
 * :class:`BatchDecoder` -- ``ntc::detail::decoder`` (netcode/detail/decoder.cc:54-152, 412-566)
@@ -106,11 +107,16 @@ class Engine:
 
 
 class GaloisField:
-    """``ntc::detail::galois_field`` for w = 8 (galois_field.hh:18-167)."""
+    """``ntc::detail::galois_field`` (galois_field.hh:18-167) for w in {4, 8, 16, 32}.
+
+    GF(2^8) uses the engine's dedicated kernels and tables (ntc_gf256_*); the other sizes the
+    generic packed shift-and-add kernels (ntc_gf_*, gf-complete's default polynomials)."""
+
+    SIZES = (4, 8, 16, 32)
 
     def __init__(self, w: int = 8, device: int | torch.device = 0):
-        if w != 8:
-            raise NotImplementedError("this build implements GF(2^8) only (w = 8)")
+        if w not in GaloisField.SIZES:
+            raise ValueError("galois field size must be 4, 8, 16 or 32")
         self.w = w
         self._L = _native.load()
         self._dev = device
@@ -119,18 +125,27 @@ class GaloisField:
         return self.w
 
     def coefficient(self, repair_id: int, src_id: int) -> int:
-        return self._L.ntc_gf256_coefficient(repair_id & 0xFFFFFFFF, src_id & 0xFFFFFFFF)
+        rid, sid = repair_id & 0xFFFFFFFF, src_id & 0xFFFFFFFF
+        if self.w == 8:
+            return self._L.ntc_gf256_coefficient(rid, sid)
+        return self._L.ntc_gf_coefficient(self.w, rid, sid)
 
     def multiply_size(self, size: int, coeff: int) -> int:
-        return self._L.ntc_gf256_multiply_size(size, coeff)
+        if self.w == 8:
+            return self._L.ntc_gf256_multiply_size(size, coeff)
+        return self._L.ntc_gf_multiply_size(self.w, size, coeff & 0xFFFFFFFF)
 
     def multiply_scalar(self, x: int, y: int) -> int:
-        return self._L.ntc_gf256_multiply(x, y)
+        if self.w == 8:
+            return self._L.ntc_gf256_multiply(x, y)
+        return self._L.ntc_gf_multiply(self.w, x & 0xFFFFFFFF, y & 0xFFFFFFFF)
 
     def invert(self, x: int) -> int:
         if x == 0:
-            raise ZeroDivisionError("0 has no inverse in GF(2^8)")
-        return self._L.ntc_gf256_invert(x)
+            raise ZeroDivisionError(f"0 has no inverse in GF(2^{self.w})")
+        if self.w == 8:
+            return self._L.ntc_gf256_invert(x)
+        return self._L.ntc_gf_invert(self.w, x & 0xFFFFFFFF)
 
     def _region(self, src: torch.Tensor, dst: torch.Tensor, length: int, coeff: int, add: int):
         if src.dtype != torch.uint8 or dst.dtype != torch.uint8:
@@ -140,10 +155,14 @@ class GaloisField:
         if length > src.numel() or length > dst.numel():
             raise ValueError("length exceeds region")
         eng = Engine.get(src.device)
-        _native.check(self._L.ntc_gf256_region_multiply(eng.handle, src.data_ptr(), dst.data_ptr(),
-                                                       length, coeff & 0xFF, add,
-                                                       _stream(src.device)),
-                      "ntc_gf256_region_multiply")
+        if self.w == 8:
+            _native.check(self._L.ntc_gf256_region_multiply(
+                eng.handle, src.data_ptr(), dst.data_ptr(), length, coeff & 0xFF, add,
+                _stream(src.device)), "ntc_gf256_region_multiply")
+        else:
+            _native.check(self._L.ntc_gf_region_multiply(
+                eng.handle, self.w, src.data_ptr(), dst.data_ptr(), length, coeff & 0xFFFFFFFF,
+                add, _stream(src.device)), "ntc_gf_region_multiply")
 
     def multiply(self, src: torch.Tensor, dst: torch.Tensor, length: int, coeff: int):
         """dst[:length] = coeff * src[:length]  (galois_field.hh:65-75)."""
@@ -152,6 +171,25 @@ class GaloisField:
     def multiply_add(self, src: torch.Tensor, dst: torch.Tensor, length: int, coeff: int):
         """dst[:length] ^= coeff * src[:length]  (galois_field.hh:83-92)."""
         self._region(src, dst, length, coeff, 1)
+
+
+def combine(w: int, inputs: torch.Tensor, coef: torch.Tensor, out: torch.Tensor | None = None):
+    """Batched combination in GF(2^w): out[g][j] = sum_i coef[g][i][j] * inputs[g][i]
+    (ntc_gf_combine_batch).  inputs [G, k, stride] uint8 (stride % 16 == 0), coef [G, k, rows]
+    int32/uint32 field elements."""
+    G, k, stride = inputs.shape
+    rows = coef.shape[2]
+    dev = inputs.device
+    _require(inputs, "inputs", _U8, (G, k, stride), dev)
+    _require(coef, "coef", _U32, (G, k, rows), dev)
+    if out is None:
+        out = torch.empty((G, rows, stride), dtype=torch.uint8, device=dev)
+    eng = Engine.get(dev)
+    _native.check(_native.load().ntc_gf_combine_batch(eng.handle, w, G, k, rows, stride,
+                                                      inputs.data_ptr(), coef.data_ptr(),
+                                                      out.data_ptr(), _stream(dev)),
+                  "ntc_gf_combine_batch")
+    return out
 
 
 @dataclass

@@ -161,9 +161,15 @@ void dispatch_and_errors()
   dec.set_ack_nb_packets(500);
   CHECK(dec.ack_nb_packets() == 128);
   CHECK(enc.galois_field_size() == 8);
-  bool unsupported = false;
-  try { ntc::encoder<packet_sink> e16{16, packet_sink{}}; } catch (const std::runtime_error&) { unsupported = true; }
-  CHECK(unsupported);
+  {  // every field size netcode supports (galois_field.hh:39); anything else is rejected
+    ntc::encoder<packet_sink> e16{16, packet_sink{}};
+    CHECK(e16.galois_field_size() == 16);
+    ntc::encoder<packet_sink> e32{32, packet_sink{}};
+    CHECK(e32.galois_field_size() == 32);
+    bool unsupported = false;
+    try { ntc::encoder<packet_sink> e7{7, packet_sink{}}; } catch (const std::runtime_error&) { unsupported = true; }
+    CHECK(unsupported);
+  }
   std::cout << "ok dispatch_and_errors\n";
 }
 

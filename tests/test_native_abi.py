@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared_symbols(header):
     txt = open(os.path.join(ROOT, "include", "netcode", header)).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(ntc_gf256_[a-z_0-9]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(ntc_gf(?:256)?_[a-z_0-9]+)\s*\(", txt)))
 
 
 def test_header_symbols_match_loader_list():

@@ -80,6 +80,9 @@ def load():
         "ntc_decoder_generate_ack": (None, [P, E]), "ntc_decoder_set_ack_period": (None, [P, S]),
         "ntc_decoder_set_ack_nb_packets": (None, [P, u16]),
         "ntc_encoder_counter": (S, [P, C.c_int]), "ntc_decoder_counter": (S, [P, C.c_int]),
+        "ntc_new_batch": (P, []), "ntc_delete_batch": (None, [P]),
+        "ntc_encoder_set_batch": (None, [P, P, E]), "ntc_batch_flush": (None, [P, E]),
+        "ntc_batch_pending": (S, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -172,10 +175,42 @@ class Encoder:
     def set_adaptive(self, a: bool):
         self.L.ntc_encoder_set_adaptive(self.h, bool(a))
 
+    def set_batch(self, batch: "Batch | None"):
+        """Attach to an online batching adaptor (None detaches; flushes the current batch)."""
+        err = Error(0, None)
+        self.L.ntc_encoder_set_batch(self.h, batch.h if batch is not None else None, C.byref(err))
+        _check(err)
+        self._batch = batch          # keep the batch alive while attached
+
     def __getattr__(self, name):
         if name in Encoder.COUNTERS:
             return self.L.ntc_encoder_counter(self.h, Encoder.COUNTERS.index(name))
         raise AttributeError(name)
+
+
+class Batch:
+    """ntc_batch_t (netcode/c/ext.h): attached encoders' packets are queued until flush(), which
+    computes every pending repair in one GPU launch per field size and emits in production order."""
+
+    def __init__(self):
+        self.L = load()
+        self.h = self.L.ntc_new_batch()
+        if not self.h:
+            raise MemoryError
+
+    def flush(self):
+        err = Error(0, None)
+        self.L.ntc_batch_flush(self.h, C.byref(err))
+        _check(err)
+
+    @property
+    def pending(self) -> int:
+        return self.L.ntc_batch_pending(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.ntc_delete_batch(self.h)
+            self.h = None
 
 
 class Decoder:

@@ -114,6 +114,41 @@ class Device {
     for (size_t s = 0; s < rows; ++s) std::memcpy(out[s], h_out_ + s * stride, out_len);
   }
 
+  // G independent combinations of up to k inputs each (batched repairs):
+  //   out_g = sum_i c_gi * in_gi, inputs from fill(g, i, &ptr, &len, &c) (false past the last),
+  //   each output handed to sink(g, bytes) -- one H2D, one launch, one D2H.
+  template <typename Fill, typename Sink>
+  void combine_generations(uint32_t w, size_t G, size_t k, size_t stride, Fill fill, Sink sink)
+  {
+    const uint32_t pitch = w == 8 ? ntc_gf256_coef_pitch(1) : 4u;
+    grow(G * k * stride, G * k * pitch, G * stride);
+    std::memset(h_coef_, 0, G * k * pitch);
+    for (size_t g = 0; g < G; ++g)
+      for (size_t i = 0; i < k; ++i) {
+        uint8_t* dst = h_in_ + (g * k + i) * stride;
+        const uint8_t* ptr = nullptr;
+        uint16_t len = 0;
+        uint32_t c = 0;
+        if (!fill(g, i, &ptr, &len, &c)) { std::memset(dst, 0, stride); continue; }
+        std::memcpy(dst, ptr, len);
+        std::memset(dst + len, 0, stride - len);
+        if (w == 8) h_coef_[(g * k + i) * pitch] = static_cast<uint8_t>(c);
+        else std::memcpy(h_coef_ + (g * k + i) * pitch, &c, 4);
+      }
+    check(hipMemcpyAsync(d_in_, h_in_, G * k * stride, hipMemcpyHostToDevice, stream_), "H2D");
+    check(hipMemcpyAsync(d_coef_, h_coef_, G * k * pitch, hipMemcpyHostToDevice, stream_), "H2D");
+    const int rc = w == 8
+        ? ntc_gf256_combine_batch(eng_, static_cast<uint32_t>(G), static_cast<uint32_t>(k), 1,
+                                  static_cast<uint32_t>(stride), d_in_, d_coef_, d_out_, stream_)
+        : ntc_gf_combine_batch(eng_, w, static_cast<uint32_t>(G), static_cast<uint32_t>(k), 1,
+                               static_cast<uint32_t>(stride), d_in_,
+                               reinterpret_cast<const uint32_t*>(d_coef_), d_out_, stream_);
+    if (rc) throw device_error(ntc_gf256_last_error());
+    check(hipMemcpyAsync(h_out_, d_out_, G * stride, hipMemcpyDeviceToHost, stream_), "D2H");
+    check(hipStreamSynchronize(stream_), "sync");
+    for (size_t g = 0; g < G; ++g) sink(g, h_out_ + g * stride);
+  }
+
   uint64_t launches() const { return launches_; }
 
  private:
@@ -201,7 +236,12 @@ struct Field {
 // Big-endian fields; id lists RLE-coded on 16-bit deltas (detail/packetizer.hh:263-352).
 struct Writer {
   ntc_packet_handler h;
-  void raw(const void* p, size_t n) { h.prepare_packet(h.context, static_cast<const char*>(p), n); }
+  bytes* buf = nullptr;        // set: packets are built into *buf instead of going to h
+  void raw(const void* p, size_t n)
+  {
+    if (buf) buf->insert(buf->end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n);
+    else h.prepare_packet(h.context, static_cast<const char*>(p), n);
+  }
   void u8(uint8_t x) { raw(&x, 1); }
   void u16(uint16_t x) { const uint8_t b[2] = {uint8_t(x >> 8), uint8_t(x)}; raw(b, 2); }
   void u32(uint32_t x)
@@ -225,7 +265,7 @@ struct Writer {
     u32(v[0]);
     for (const auto& p : rle) { u8(p.first); u16(p.second); }
   }
-  void end() { h.send_packet(h.context); }
+  void end() { if (!buf) h.send_packet(h.context); }
 };
 
 struct Reader {
@@ -276,24 +316,46 @@ struct ntc_packet_t {
 namespace ntcx {
 
 // ============================================================================== encoder ====
+class Batch;
+using sym_ptr = std::shared_ptr<const bytes>;
+
+// A packet an encoder attached to a Batch has produced but not yet emitted.  Repairs keep the
+// window as it was (shared source symbols + coefficients); their two symbol copies are filled in
+// at flush time.
+struct Pending {
+  class Encoder* enc;
+  bytes pkt;                           // complete wire bytes (repair symbols zero until flush)
+  bool repair = false;
+  uint32_t w = 8;
+  std::vector<sym_ptr> srcs;
+  std::vector<uint32_t> coefs;
+  uint16_t symsz = 0;
+  size_t off1 = 0, off2 = 0;           // the two symbol copies inside pkt
+};
+
 class Encoder {
  public:
   Encoder(uint8_t w, ntc_packet_handler h) : f_(w), out_{h} { Device::get(); }
+  Encoder(Encoder&&) = default;
+  ~Encoder();
 
   // encoder.hh:255-285
   void add_data(bytes&& d)
   {
     if (window_.size() == window_size_) window_.pop_front();
-    window_.push_back(Src{cur_sid_, std::move(d)});
+    window_.push_back(Src{cur_sid_, std::make_shared<const bytes>(std::move(d))});
     const Src& s = window_.back();
     if (systematic_) {
       ++nb_sources_;
       ++nb_sent_packets_;
+      Pending p{this};
+      begin(p);
       out_.u8(2);                                  // packetizer.hh:165-183
       out_.u32(s.id);
-      out_.u16(static_cast<uint16_t>(s.sym.size()));
-      out_.raw(s.sym.data(), s.sym.size());
+      out_.u16(static_cast<uint16_t>(s.sym->size()));
+      out_.raw(s.sym->data(), s.sym->size());
       out_.end();
+      finish(std::move(p));
     } else {
       generate_repair();
     }
@@ -301,7 +363,8 @@ class Encoder {
     ++cur_sid_;
   }
 
-  // encoder.hh:162-169, 321-333 + detail/encoder.cc:15-64 (the combination runs on the GPU)
+  // encoder.hh:162-169, 321-333 + detail/encoder.cc:15-64 (the combination runs on the GPU; with
+  // a Batch attached it is deferred to the batch's flush, one launch for every pending repair)
   void generate_repair()
   {
     if (window_.empty()) throw std::runtime_error("generate_repair on an empty window");
@@ -309,31 +372,51 @@ class Encoder {
     std::vector<uint16_t> lens;
     std::vector<uint32_t> cs;
     std::vector<uint32_t> ids;
+    std::vector<sym_ptr> srcs;
     uint16_t symsz = 0, esz = 0;
     for (const Src& s : window_) {
       const uint32_t c = f_.coef(cur_rid_, s.id);
-      in.push_back(s.sym.data());
-      lens.push_back(static_cast<uint16_t>(s.sym.size()));
+      in.push_back(s.sym->data());
+      lens.push_back(static_cast<uint16_t>(s.sym->size()));
       cs.push_back(c);
       ids.push_back(s.id);
-      symsz = std::max<uint16_t>(symsz, static_cast<uint16_t>(s.sym.size()));
-      esz = static_cast<uint16_t>(f_.msize(static_cast<uint16_t>(s.sym.size()), c) ^ esz);
+      if (batch_) srcs.push_back(s.sym);
+      symsz = std::max<uint16_t>(symsz, static_cast<uint16_t>(s.sym->size()));
+      esz = static_cast<uint16_t>(f_.msize(static_cast<uint16_t>(s.sym->size()), c) ^ esz);
     }
     bytes sym(symsz);
-    Device::get().combine(f_.w, in.size(), in.data(), lens.data(), cs.data(), symsz, sym.data());
+    if (!batch_)
+      Device::get().combine(f_.w, in.size(), in.data(), lens.data(), cs.data(), symsz, sym.data());
     const uint32_t rid = cur_rid_++;
     ++nb_repairs_;
     ++nb_sent_packets_;
+    Pending p{this};
+    begin(p);
     out_.u8(1);                                    // packetizer.hh:90-122
     out_.u32(rid);
     out_.u16(symsz);
+    p.off1 = p.pkt.size();
     out_.raw(sym.data(), symsz);
     out_.ids(ids);
     out_.u16(esz);
     out_.u16(symsz);
+    p.off2 = p.pkt.size();
     out_.raw(sym.data(), symsz);
     out_.end();
+    if (batch_) {
+      p.repair = true;
+      p.w = f_.w;
+      p.srcs = std::move(srcs);
+      p.coefs = std::move(cs);
+      p.symsz = symsz;
+    }
+    finish(std::move(p));
   }
+
+  void set_batch(Batch* b);
+  void drop_batch() { batch_ = nullptr; }
+  Batch* batch() const { return batch_; }
+  const ntc_packet_handler& handler() const { return out_.h; }
 
   // encoder.hh:290-318 + packetizer.hh:64-88 + source_list.hh:34-60
   size_t add_packet(const uint8_t* p, size_t n)
@@ -382,10 +465,15 @@ class Encoder {
  private:
   struct Src {
     uint32_t id;
-    bytes sym;
+    sym_ptr sym;                       // immutable once in the window (shared with pending repairs)
   };
+  // batch mode: the packet is built into p.pkt (begin) and queued in the batch (finish)
+  void begin(Pending& p) { out_.buf = batch_ ? &p.pkt : nullptr; }
+  void finish(Pending&& p);
+
   Field f_;
   Writer out_;
+  Batch* batch_ = nullptr;
   std::list<Src> window_;
   size_t rate_ = 5;
   size_t window_size_ = static_cast<size_t>(-1);
@@ -395,6 +483,98 @@ class Encoder {
   size_t nb_repairs_ = 0, nb_acks_ = 0, nb_sources_ = 0;
   uint16_t nb_sent_packets_ = 0;
 };
+
+// ============================================================================ batching ====
+// an online batching adaptor behind the per-packet encoder.  Encoders attached
+// to a Batch queue every packet they produce (sources and repairs, in production order, so every
+// encoder's packet sequence is exactly the unbatched one); flush() computes all pending repairs of
+// all attached encoders with one combine launch per field size -- instead of one launch and one
+// PCIe round trip per repair -- then emits the queued packets in production order.
+class Batch {
+ public:
+  ~Batch()
+  {
+    for (Encoder* e : encs_) e->drop_batch();   // pending packets are discarded
+  }
+  void attach(Encoder* e) { encs_.push_back(e); }
+  void detach(Encoder* e)
+  {
+    encs_.erase(std::remove(encs_.begin(), encs_.end(), e), encs_.end());
+    q_.erase(std::remove_if(q_.begin(), q_.end(), [e](const Pending& p) { return p.enc == e; }),
+             q_.end());
+  }
+  void push(Pending&& p) { q_.push_back(std::move(p)); }
+  size_t pending() const { return q_.size(); }
+
+  void flush()
+  {
+    for (uint32_t w : {4u, 8u, 16u, 32u}) compute(w);
+    std::vector<Pending> q;
+    q.swap(q_);                         // handlers may queue again (they may not, but be safe)
+    for (const Pending& p : q) {
+      const ntc_packet_handler& h = p.enc->handler();
+      h.prepare_packet(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.pkt.size());
+      h.send_packet(h.context);
+    }
+  }
+
+ private:
+  // every pending repair of field w: one [n][kmax][stride] combine, symbols copied into packets
+  void compute(uint32_t w)
+  {
+    std::vector<Pending*> reps;
+    size_t kmax = 0, mx = 16;
+    for (Pending& p : q_) {
+      if (!p.repair || p.w != w) continue;
+      reps.push_back(&p);
+      kmax = std::max(kmax, p.srcs.size());
+      mx = std::max<size_t>(mx, p.symsz);
+    }
+    if (reps.empty()) return;
+    const size_t stride = (mx + 15) / 16 * 16;
+    Device::get().combine_generations(w, reps.size(), kmax, stride, [&](size_t g, size_t i,
+                                                                        const uint8_t** ptr,
+                                                                        uint16_t* len, uint32_t* c) {
+      const Pending& p = *reps[g];
+      if (i >= p.srcs.size()) return false;
+      *ptr = p.srcs[i]->data();
+      *len = static_cast<uint16_t>(p.srcs[i]->size());
+      *c = p.coefs[i];
+      return true;
+    }, [&](size_t g, const uint8_t* sym) {
+      Pending& p = *reps[g];
+      std::memcpy(p.pkt.data() + p.off1, sym, p.symsz);
+      std::memcpy(p.pkt.data() + p.off2, sym, p.symsz);
+      p.repair = false;                 // computed (a failed flush can be retried)
+      p.srcs.clear();                   // release the window snapshot
+    });
+  }
+
+  std::vector<Encoder*> encs_;
+  std::vector<Pending> q_;
+};
+
+Encoder::~Encoder()
+{
+  if (batch_) batch_->detach(this);
+}
+
+void Encoder::set_batch(Batch* b)
+{
+  if (b == batch_) return;
+  if (batch_) {
+    batch_->flush();                    // keep this encoder's packet order across the switch
+    batch_->detach(this);
+  }
+  batch_ = b;
+  if (b) b->attach(this);
+}
+
+void Encoder::finish(Pending&& p)
+{
+  out_.buf = nullptr;
+  if (batch_) batch_->push(std::move(p));
+}
 
 // ============================================================================== decoder ====
 // detail/decoder.{hh,cc} semantics; host containers, GPU region work.
@@ -808,6 +988,9 @@ auto guarded(Fn&& fn, ntc_error* error) noexcept -> decltype(fn())
 struct ntc_encoder_t {
   ntcx::Encoder e;
 };
+struct ntc_batch_t {
+  ntcx::Batch b;
+};
 struct ntc_decoder_t {
   ntcx::Decoder d;
 };
@@ -918,5 +1101,20 @@ void ntc_decoder_set_ack_nb_packets(ntc_decoder_t* dec, uint16_t nb) noexcept { 
 // ---------------------------------------------------------------- extensions (ext.h) ----
 size_t ntc_encoder_counter(const ntc_encoder_t* enc, int which) noexcept { return enc->e.counter(which); }
 size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) noexcept { return dec->d.counter(which); }
+
+ntc_batch_t* ntc_new_batch(void) noexcept
+{
+  try { return new ntc_batch_t{}; } catch (...) { return nullptr; }
+}
+void ntc_delete_batch(ntc_batch_t* b) noexcept { delete b; }
+void ntc_encoder_set_batch(ntc_encoder_t* enc, ntc_batch_t* b, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { enc->e.set_batch(b ? &b->b : nullptr); }, error);
+}
+void ntc_batch_flush(ntc_batch_t* b, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { b->b.flush(); }, error);
+}
+size_t ntc_batch_pending(const ntc_batch_t* b) noexcept { return b->b.pending(); }
 
 }  // extern "C"

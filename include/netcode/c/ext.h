@@ -22,19 +22,23 @@ enum {
 size_t ntc_encoder_counter(const ntc_encoder_t* enc, int which) NTC_C_NOEXCEPT NTC_C_NONNULL;
 size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT NTC_C_NONNULL;
 
-/* Online batching adaptor.  Encoders attached to a batch queue every packet
- * they produce instead of calling their packet handler; ntc_batch_flush computes every pending
- * repair of every attached encoder with one GPU launch per Galois field size, then calls the
- * handlers for all queued packets in production order (each packet as one prepare_packet call
- * followed by send_packet).  Each encoder's packet sequence is byte-for-byte the unbatched one
- * (encoder.hh:255-333 semantics; counters, window and rate update immediately); only the time of
- * the callbacks moves to the flush.  Attaching an encoder to another batch or to NULL flushes its
- * current batch first.  Deleting an attached encoder discards its queued packets; deleting a
- * batch discards every queued packet and detaches its encoders. */
+/* Online batching adaptor.  Encoders and decoders attached to a batch queue
+ * every packet and data delivery they produce instead of calling their handlers.  Their protocol
+ * state (windows, rates, counters, missing / pending sets, acks) advances immediately -- the
+ * reference's control flow never depends on payload bytes -- while each GF region result is kept
+ * as a linear expression over the payloads it came from.  ntc_batch_flush evaluates every pending
+ * expression (encoder repairs, decoder deliveries) with one GPU launch per Galois field size, then
+ * calls the handlers in production order (a packet as one prepare_packet call followed by
+ * send_packet).  Each object's callback sequence is byte-for-byte the unbatched one
+ * (encoder.hh:255-333, decoder.hh:88-300 semantics); only the time of the callbacks moves to the
+ * flush.  Attaching an object to another batch or to NULL flushes its current batch first.
+ * Deleting an attached object discards its queued events; deleting a batch discards every queued
+ * event and detaches its objects. */
 typedef struct ntc_batch_t ntc_batch_t;
 ntc_batch_t* ntc_new_batch(void) NTC_C_NOEXCEPT;
 void ntc_delete_batch(ntc_batch_t* batch) NTC_C_NOEXCEPT NTC_C_NONNULL;
 void ntc_encoder_set_batch(ntc_encoder_t* enc, ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT;
+void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT;
 void ntc_batch_flush(ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT NTC_C_NONNULL;
 size_t ntc_batch_pending(const ntc_batch_t* batch) NTC_C_NOEXCEPT NTC_C_NONNULL;
 

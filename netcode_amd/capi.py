@@ -81,7 +81,8 @@ def load():
         "ntc_decoder_set_ack_nb_packets": (None, [P, u16]),
         "ntc_encoder_counter": (S, [P, C.c_int]), "ntc_decoder_counter": (S, [P, C.c_int]),
         "ntc_new_batch": (P, []), "ntc_delete_batch": (None, [P]),
-        "ntc_encoder_set_batch": (None, [P, P, E]), "ntc_batch_flush": (None, [P, E]),
+        "ntc_encoder_set_batch": (None, [P, P, E]), "ntc_decoder_set_batch": (None, [P, P, E]),
+        "ntc_batch_flush": (None, [P, E]),
         "ntc_batch_pending": (S, [P]),
     }
     for name, (res, args) in sig.items():
@@ -252,6 +253,13 @@ class Decoder:
             self.L.ntc_delete_packet(p)
         _check(err)
         return n
+
+    def set_batch(self, batch: "Batch | None"):
+        """Attach to an online batching adaptor (None detaches; flushes the current batch)."""
+        err = Error(0, None)
+        self.L.ntc_decoder_set_batch(self.h, batch.h if batch is not None else None, C.byref(err))
+        _check(err)
+        self._batch = batch
 
     def generate_ack(self):
         err = Error(0, None)

@@ -318,19 +318,44 @@ namespace ntcx {
 // ============================================================================== encoder ====
 class Batch;
 using sym_ptr = std::shared_ptr<const bytes>;
+class Decoder;
 
-// A packet an encoder attached to a Batch has produced but not yet emitted.  Repairs keep the
-// window as it was (shared source symbols + coefficients); their two symbol copies are filled in
-// at flush time.
+// Deferred (batched) symbols are linear expressions over received / produced payloads:
+// sum of c * (the first `len` bytes of *base, zero-extended).  Addition in GF(2^w) is XOR, so
+// terms over the same (base, len) merge by XOR-ing their coefficients.
+struct Term {
+  sym_ptr base;
+  uint32_t c;
+  uint16_t len;
+};
+using Expr = std::vector<Term>;
+
+void expr_add(Expr& dst, const Term& t)
+{
+  if (t.c == 0 || t.len == 0) return;
+  for (auto it = dst.begin(); it != dst.end(); ++it)
+    if (it->base == t.base && it->len == t.len) {
+      it->c ^= t.c;
+      if (it->c == 0) dst.erase(it);
+      return;
+    }
+  dst.push_back(t);
+}
+
+// One event queued in a Batch, emitted at flush in production order: a packet (encoder source,
+// encoder repair whose two symbol copies are filled at flush, decoder ack) or a decoder data
+// delivery (its bytes = expr evaluated at flush, truncated to `size`).
 struct Pending {
-  class Encoder* enc;
-  bytes pkt;                           // complete wire bytes (repair symbols zero until flush)
-  bool repair = false;
+  enum Kind { ENC_PACKET, DEC_PACKET, DEC_DATA };
+  Kind kind = ENC_PACKET;
+  class Encoder* enc = nullptr;
+  class Decoder* dec = nullptr;
+  bytes pkt;                           // wire bytes, or the delivered data
+  bool eval = false;                   // expr still to be evaluated
   uint32_t w = 8;
-  std::vector<sym_ptr> srcs;
-  std::vector<uint32_t> coefs;
-  uint16_t symsz = 0;
-  size_t off1 = 0, off2 = 0;           // the two symbol copies inside pkt
+  Expr expr;
+  uint16_t size = 0;                   // evaluated length (repair symbol size / data size)
+  size_t off1 = 0, off2 = 0;           // encoder repair: the two symbol copies inside pkt
 };
 
 class Encoder {
@@ -348,7 +373,8 @@ class Encoder {
     if (systematic_) {
       ++nb_sources_;
       ++nb_sent_packets_;
-      Pending p{this};
+      Pending p;
+      p.enc = this;
       begin(p);
       out_.u8(2);                                  // packetizer.hh:165-183
       out_.u32(s.id);
@@ -372,7 +398,7 @@ class Encoder {
     std::vector<uint16_t> lens;
     std::vector<uint32_t> cs;
     std::vector<uint32_t> ids;
-    std::vector<sym_ptr> srcs;
+    Expr terms;
     uint16_t symsz = 0, esz = 0;
     for (const Src& s : window_) {
       const uint32_t c = f_.coef(cur_rid_, s.id);
@@ -380,7 +406,7 @@ class Encoder {
       lens.push_back(static_cast<uint16_t>(s.sym->size()));
       cs.push_back(c);
       ids.push_back(s.id);
-      if (batch_) srcs.push_back(s.sym);
+      if (batch_) expr_add(terms, Term{s.sym, c, static_cast<uint16_t>(s.sym->size())});
       symsz = std::max<uint16_t>(symsz, static_cast<uint16_t>(s.sym->size()));
       esz = static_cast<uint16_t>(f_.msize(static_cast<uint16_t>(s.sym->size()), c) ^ esz);
     }
@@ -390,7 +416,8 @@ class Encoder {
     const uint32_t rid = cur_rid_++;
     ++nb_repairs_;
     ++nb_sent_packets_;
-    Pending p{this};
+    Pending p;
+    p.enc = this;
     begin(p);
     out_.u8(1);                                    // packetizer.hh:90-122
     out_.u32(rid);
@@ -404,11 +431,10 @@ class Encoder {
     out_.raw(sym.data(), symsz);
     out_.end();
     if (batch_) {
-      p.repair = true;
+      p.eval = true;
       p.w = f_.w;
-      p.srcs = std::move(srcs);
-      p.coefs = std::move(cs);
-      p.symsz = symsz;
+      p.expr = std::move(terms);
+      p.size = symsz;
     }
     finish(std::move(p));
   }
@@ -484,98 +510,6 @@ class Encoder {
   uint16_t nb_sent_packets_ = 0;
 };
 
-// ============================================================================ batching ====
-// an online batching adaptor behind the per-packet encoder.  Encoders attached
-// to a Batch queue every packet they produce (sources and repairs, in production order, so every
-// encoder's packet sequence is exactly the unbatched one); flush() computes all pending repairs of
-// all attached encoders with one combine launch per field size -- instead of one launch and one
-// PCIe round trip per repair -- then emits the queued packets in production order.
-class Batch {
- public:
-  ~Batch()
-  {
-    for (Encoder* e : encs_) e->drop_batch();   // pending packets are discarded
-  }
-  void attach(Encoder* e) { encs_.push_back(e); }
-  void detach(Encoder* e)
-  {
-    encs_.erase(std::remove(encs_.begin(), encs_.end(), e), encs_.end());
-    q_.erase(std::remove_if(q_.begin(), q_.end(), [e](const Pending& p) { return p.enc == e; }),
-             q_.end());
-  }
-  void push(Pending&& p) { q_.push_back(std::move(p)); }
-  size_t pending() const { return q_.size(); }
-
-  void flush()
-  {
-    for (uint32_t w : {4u, 8u, 16u, 32u}) compute(w);
-    std::vector<Pending> q;
-    q.swap(q_);                         // handlers may queue again (they may not, but be safe)
-    for (const Pending& p : q) {
-      const ntc_packet_handler& h = p.enc->handler();
-      h.prepare_packet(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.pkt.size());
-      h.send_packet(h.context);
-    }
-  }
-
- private:
-  // every pending repair of field w: one [n][kmax][stride] combine, symbols copied into packets
-  void compute(uint32_t w)
-  {
-    std::vector<Pending*> reps;
-    size_t kmax = 0, mx = 16;
-    for (Pending& p : q_) {
-      if (!p.repair || p.w != w) continue;
-      reps.push_back(&p);
-      kmax = std::max(kmax, p.srcs.size());
-      mx = std::max<size_t>(mx, p.symsz);
-    }
-    if (reps.empty()) return;
-    const size_t stride = (mx + 15) / 16 * 16;
-    Device::get().combine_generations(w, reps.size(), kmax, stride, [&](size_t g, size_t i,
-                                                                        const uint8_t** ptr,
-                                                                        uint16_t* len, uint32_t* c) {
-      const Pending& p = *reps[g];
-      if (i >= p.srcs.size()) return false;
-      *ptr = p.srcs[i]->data();
-      *len = static_cast<uint16_t>(p.srcs[i]->size());
-      *c = p.coefs[i];
-      return true;
-    }, [&](size_t g, const uint8_t* sym) {
-      Pending& p = *reps[g];
-      std::memcpy(p.pkt.data() + p.off1, sym, p.symsz);
-      std::memcpy(p.pkt.data() + p.off2, sym, p.symsz);
-      p.repair = false;                 // computed (a failed flush can be retried)
-      p.srcs.clear();                   // release the window snapshot
-    });
-  }
-
-  std::vector<Encoder*> encs_;
-  std::vector<Pending> q_;
-};
-
-Encoder::~Encoder()
-{
-  if (batch_) batch_->detach(this);
-}
-
-void Encoder::set_batch(Batch* b)
-{
-  if (b == batch_) return;
-  if (batch_) {
-    batch_->flush();                    // keep this encoder's packet order across the switch
-    batch_->detach(this);
-  }
-  batch_ = b;
-  if (b) b->attach(this);
-}
-
-void Encoder::finish(Pending&& p)
-{
-  out_.buf = nullptr;
-  if (batch_) batch_->push(std::move(p));
-}
-
 // ============================================================================== decoder ====
 // detail/decoder.{hh,cc} semantics; host containers, GPU region work.
 class Decoder {
@@ -585,6 +519,13 @@ class Decoder {
   {
     Device::get();
   }
+  Decoder(Decoder&&) = default;
+  ~Decoder();
+
+  void set_batch(Batch* b);
+  void drop_batch() { batch_ = nullptr; }
+  const ntc_packet_handler& packet_handler() const { return out_.h; }
+  const ntc_data_handler& data_handler() const { return dh_; }
 
   // decoder.hh:88-122
   size_t add_packet(const uint8_t* p, size_t n)
@@ -623,10 +564,16 @@ class Decoder {
     std::vector<uint32_t> ids;
     ids.reserve(sources_.size());
     for (const auto& kv : sources_) ids.push_back(kv.first);
+    Pending p;
+    p.kind = Pending::DEC_PACKET;
+    p.dec = this;
+    out_.buf = batch_ ? &p.pkt : nullptr;
     out_.u8(0);
     out_.u16(ack_packets_);
     out_.ids(ids);
     out_.end();
+    out_.buf = nullptr;
+    queue(std::move(p));
     ++nb_acks_;
     ack_packets_ = 0;
   }
@@ -654,6 +601,7 @@ class Decoder {
     uint32_t id;
     bytes sym;
     uint16_t size;
+    Expr expr;                   // batch mode: the symbol as an expression (sym unused)
   };
   struct Rep {
     uint32_t id;
@@ -661,12 +609,61 @@ class Decoder {
     uint16_t esz;
     bytes sym;
     uint16_t symsz;
+    Expr expr;
   };
+
+  void queue(Pending&& p);
+  // evaluate expressions into byte symbols (leaving batch mode): one combine for all of them
+  void materialise(const std::vector<std::pair<Expr*, bytes*>>& todo, const std::vector<uint16_t>& lens)
+  {
+    size_t kmax = 1, mx = 16;
+    for (size_t g = 0; g < todo.size(); ++g) {
+      kmax = std::max(kmax, todo[g].first->size());
+      mx = std::max<size_t>(mx, lens[g]);
+      for (const Term& t : *todo[g].first) mx = std::max<size_t>(mx, t.len);
+    }
+    if (!todo.empty())
+      Device::get().combine_generations(f_.w, todo.size(), kmax, (mx + 15) / 16 * 16,
+          [&](size_t g, size_t i, const uint8_t** ptr, uint16_t* len, uint32_t* c) {
+            const Expr& e = *todo[g].first;
+            if (i >= e.size()) return false;
+            *ptr = e[i].base->data();
+            *len = e[i].len;
+            *c = e[i].c;
+            return true;
+          },
+          [&](size_t g, const uint8_t* sym) {
+            todo[g].second->assign(sym, sym + std::max<uint16_t>(lens[g], 1));
+            if (lens[g] == 0) (*todo[g].second)[0] = 0;
+            todo[g].first->clear();
+          });
+  }
+  // batch mode: c * (src truncated to len), added into dst
+  void add_scaled(Expr& dst, const Expr& src, uint32_t c, uint16_t len) const
+  {
+    for (const Term& t : src) expr_add(dst, Term{t.base, f_.mul(t.c, c), std::min(t.len, len)});
+  }
 
   // decoder.hh:231-248, 292-300
   void deliver(const Src& s)
   {
-    dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.sym.data()), s.size);
+    if (batch_) {
+      Pending p;
+      p.kind = Pending::DEC_DATA;
+      p.dec = this;
+      p.w = f_.w;
+      p.size = s.size;
+      if (s.expr.size() == 1 && s.expr[0].c == 1 && s.expr[0].len >= s.size) {
+        // a received source: its own payload, no region work
+        p.pkt.assign(s.expr[0].base->begin(), s.expr[0].base->begin() + s.size);
+      } else {
+        p.eval = true;
+        add_scaled(p.expr, s.expr, 1, s.size);
+      }
+      queue(std::move(p));
+    } else {
+      dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.sym.data()), s.size);
+    }
     if (ack_packets_ >= ack_nb_packets_) {
       generate_ack();
       last_ack_ = std::chrono::steady_clock::now();
@@ -701,6 +698,14 @@ class Decoder {
   void remove_sources_data(Rep& r, const std::vector<const Src*>& known)
   {
     if (known.empty()) return;
+    if (batch_) {
+      for (const Src* s : known) {
+        const uint32_t c = f_.coef(r.id, s->id);
+        r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
+        add_scaled(r.expr, s->expr, c, std::min<uint16_t>(s->size, r.symsz));
+      }
+      return;
+    }
     std::vector<const uint8_t*> in{r.sym.data()};
     std::vector<uint16_t> lens{r.symsz};
     std::vector<uint32_t> cs{1};
@@ -720,6 +725,12 @@ class Decoder {
     const uint32_t sid = r.ids.front();
     const uint32_t inv = f_.inv(f_.coef(r.id, sid));
     const uint16_t sz = f_.msize(r.esz, inv);
+    if (batch_) {
+      Src s{sid, bytes(), sz, {}};
+      add_scaled(s.expr, r.expr, inv, std::min(sz, r.symsz));
+      nb_decoded_ += 1;
+      return s;
+    }
     Src s{sid, bytes(std::max<size_t>(sz, 1), 0), sz};
     const uint8_t* in = r.sym.data();
     const uint16_t len = std::min(sz, r.symsz);
@@ -733,7 +744,9 @@ class Decoder {
   {
     if (has_last_ && id < last_id_) return;
     if (sources_.count(id)) return;
-    Src s{id, bytes(sym, sym + sz), sz};
+    Src s{id, bytes(), sz, {}};
+    if (batch_) s.expr.push_back(Term{std::make_shared<const bytes>(sym, sym + sz), 1, sz});
+    else s.sym.assign(sym, sym + sz);
     if (s.sym.empty()) s.sym.resize(1);
     add_source_recursive(std::move(s));
     attempt_full_decoding();
@@ -748,7 +761,9 @@ class Decoder {
     bool useless = true;
     for (uint32_t sid : ids) if (!sources_.count(sid)) { useless = false; break; }
     if (useless) { ++nb_useless_; return; }
-    Rep& r = repairs_.emplace(id, Rep{id, std::move(ids), esz, bytes(sym, sym + symsz), symsz}).first->second;
+    Rep& r = repairs_.emplace(id, Rep{id, std::move(ids), esz, bytes(), symsz, {}}).first->second;
+    if (batch_) r.expr.push_back(Term{std::make_shared<const bytes>(sym, sym + symsz), 1, symsz});
+    else r.sym.assign(sym, sym + symsz);
     if (r.sym.empty()) r.sym.resize(1);
     std::vector<const Src*> known;
     std::vector<uint32_t> remaining;
@@ -867,6 +882,22 @@ class Decoder {
     return true;
   }
 
+  // detail/decoder.cc:536-559: store a fully decoded source and deliver it (in order or not)
+  void insert_decoded(Src&& src)
+  {
+    const uint32_t sid = src.id;
+    sources_.emplace(sid, std::move(src));
+    if (!in_order_) {
+      deliver_id(sid);
+    } else if (sid == first_missing_) {
+      deliver_id(sid);
+      first_missing_ += 1;
+      flush_ordered();
+    } else {
+      ordered_.insert(sid);
+    }
+  }
+
   // detail/decoder.cc:412-566
   void attempt_full_decoding()
   {
@@ -896,6 +927,18 @@ class Decoder {
         const uint32_t c = inv[s * n + q];
         if (c) sizes[s] = static_cast<uint16_t>(f_.msize(reps[q]->esz, c) ^ sizes[s]);
       }
+    if (batch_) {                      // expressions; evaluated at the batch's flush
+      for (size_t s = 0; s < n; ++s) {
+        Src src{mids[s], bytes(1, 0), sizes[s], {}};
+        for (size_t q = 0; q < n; ++q)
+          add_scaled(src.expr, reps[q]->expr, inv[s * n + q], std::min(sizes[s], reps[q]->symsz));
+        insert_decoded(std::move(src));
+      }
+      nb_decoded_ += n;
+      repairs_.clear();
+      missing_.clear();
+      return;
+    }
     std::vector<Src> dec(n);
     std::vector<uint8_t*> outs(n);
     uint16_t mx = 0;
@@ -920,17 +963,7 @@ class Decoder {
     for (size_t s = 0; s < n; ++s) {
       // the reference reads min(src_sz, repair.symbol_size()) bytes of each repair (:523, :531)
       std::memcpy(dec[s].sym.data(), full[s].data(), sizes[s]);
-      const uint32_t sid = dec[s].id;
-      sources_.emplace(sid, std::move(dec[s]));
-      if (!in_order_) {
-        deliver_id(sid);
-      } else if (sid == first_missing_) {
-        deliver_id(sid);
-        first_missing_ += 1;
-        flush_ordered();
-      } else {
-        ordered_.insert(sid);
-      }
+      insert_decoded(std::move(dec[s]));
     }
     nb_decoded_ += n;
     repairs_.clear();
@@ -938,6 +971,7 @@ class Decoder {
   }
 
   Field f_;
+  Batch* batch_ = nullptr;
   bool in_order_;
   Writer out_;
   ntc_data_handler dh_;
@@ -955,6 +989,162 @@ class Decoder {
   size_t ack_period_ms_ = 100;
   std::chrono::steady_clock::time_point last_ack_;
 };
+
+// ============================================================================ batching ====
+// an online batching adaptor behind the per-packet encoder and decoder.
+// Objects attached to a Batch queue every packet and data delivery they produce, in production
+// order; their protocol state advances immediately (the reference's control flow never reads
+// payload bytes), while every GF region result is kept as an expression over the payloads it came
+// from.  flush() evaluates all pending expressions -- encoder repairs and decoder deliveries --
+// with one combine launch per field size instead of one launch and one PCIe round trip per region
+// operation, then emits the queue in order.  Each object's callback sequence is exactly the
+// unbatched one; only the time of the callbacks moves to the flush.
+class Batch {
+ public:
+  ~Batch();
+  void attach(Encoder* e) { encs_.push_back(e); }
+  void attach(Decoder* d) { decs_.push_back(d); }
+  void detach(Encoder* e)
+  {
+    encs_.erase(std::remove(encs_.begin(), encs_.end(), e), encs_.end());
+    q_.erase(std::remove_if(q_.begin(), q_.end(), [e](const Pending& p) { return p.enc == e; }),
+             q_.end());
+  }
+  void detach(Decoder* d)
+  {
+    decs_.erase(std::remove(decs_.begin(), decs_.end(), d), decs_.end());
+    q_.erase(std::remove_if(q_.begin(), q_.end(), [d](const Pending& p) { return p.dec == d; }),
+             q_.end());
+  }
+  void push(Pending&& p) { q_.push_back(std::move(p)); }
+  size_t pending() const { return q_.size(); }
+  void flush();
+
+ private:
+  // every pending expression of field w: one [n][kmax][stride] combine
+  void compute(uint32_t w)
+  {
+    std::vector<Pending*> jobs;
+    size_t kmax = 0, mx = 16;
+    for (Pending& p : q_) {
+      if (!p.eval || p.w != w) continue;
+      jobs.push_back(&p);
+      kmax = std::max(kmax, p.expr.size());
+      mx = std::max<size_t>(mx, p.size);
+      for (const Term& t : p.expr) mx = std::max<size_t>(mx, t.len);
+    }
+    if (jobs.empty()) return;
+    kmax = std::max<size_t>(kmax, 1);
+    const size_t stride = (mx + 15) / 16 * 16;
+    Device::get().combine_generations(w, jobs.size(), kmax, stride, [&](size_t g, size_t i,
+                                                                        const uint8_t** ptr,
+                                                                        uint16_t* len, uint32_t* c) {
+      const Pending& p = *jobs[g];
+      if (i >= p.expr.size()) return false;
+      *ptr = p.expr[i].base->data();
+      *len = p.expr[i].len;
+      *c = p.expr[i].c;
+      return true;
+    }, [&](size_t g, const uint8_t* sym) {
+      Pending& p = *jobs[g];
+      if (p.kind == Pending::ENC_PACKET) {
+        std::memcpy(p.pkt.data() + p.off1, sym, p.size);
+        std::memcpy(p.pkt.data() + p.off2, sym, p.size);
+      } else {
+        p.pkt.assign(sym, sym + p.size);
+      }
+      p.eval = false;                   // computed (a failed flush can be retried)
+      p.expr.clear();                   // release the payload snapshot
+    });
+  }
+
+  std::vector<Encoder*> encs_;
+  std::vector<Decoder*> decs_;
+  std::vector<Pending> q_;
+};
+
+Encoder::~Encoder()
+{
+  if (batch_) batch_->detach(this);
+}
+
+void Encoder::set_batch(Batch* b)
+{
+  if (b == batch_) return;
+  if (batch_) {
+    batch_->flush();                    // keep this encoder's packet order across the switch
+    batch_->detach(this);
+  }
+  batch_ = b;
+  if (b) b->attach(this);
+}
+
+void Encoder::finish(Pending&& p)
+{
+  out_.buf = nullptr;
+  if (batch_) batch_->push(std::move(p));
+}
+
+Decoder::~Decoder()
+{
+  if (batch_) batch_->detach(this);
+}
+
+void Decoder::set_batch(Batch* b)
+{
+  if (b == batch_) return;
+  if (batch_) {
+    batch_->flush();
+    batch_->detach(this);
+  }
+  if (!b) {
+    // back to immediate mode: materialise the symbols the protocol state still holds
+    std::vector<std::pair<Expr*, bytes*>> todo;
+    std::vector<uint16_t> lens;
+    for (auto& kv : sources_) { todo.push_back({&kv.second.expr, &kv.second.sym}); lens.push_back(kv.second.size); }
+    for (auto& kv : repairs_) { todo.push_back({&kv.second.expr, &kv.second.sym}); lens.push_back(kv.second.symsz); }
+    materialise(todo, lens);
+  } else {
+    // into batch mode: the held symbols become base payloads
+    for (auto& kv : sources_)
+      if (kv.second.expr.empty() && kv.second.size)
+        kv.second.expr.push_back(Term{std::make_shared<const bytes>(kv.second.sym.begin(), kv.second.sym.begin() + kv.second.size), 1, kv.second.size});
+    for (auto& kv : repairs_)
+      if (kv.second.expr.empty() && kv.second.symsz)
+        kv.second.expr.push_back(Term{std::make_shared<const bytes>(kv.second.sym.begin(), kv.second.sym.begin() + kv.second.symsz), 1, kv.second.symsz});
+  }
+  batch_ = b;
+  if (b) b->attach(this);
+}
+
+void Decoder::queue(Pending&& p)
+{
+  if (batch_) batch_->push(std::move(p));
+}
+
+Batch::~Batch()
+{
+  for (Encoder* e : encs_) e->drop_batch();      // pending events are discarded
+  for (Decoder* d : decs_) d->drop_batch();
+}
+
+void Batch::flush()
+{
+  for (uint32_t w : {4u, 8u, 16u, 32u}) compute(w);
+  std::vector<Pending> q;
+  q.swap(q_);
+  for (const Pending& p : q) {
+    if (p.kind == Pending::DEC_DATA) {
+      const ntc_data_handler& h = p.dec->data_handler();
+      h.read_data(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.size);
+      continue;
+    }
+    const ntc_packet_handler& h = p.kind == Pending::ENC_PACKET ? p.enc->handler()
+                                                                : p.dec->packet_handler();
+    h.prepare_packet(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.pkt.size());
+    h.send_packet(h.context);
+  }
+}
 
 // c/detail/check_error.hh: exceptions -> ntc_error (message in thread-local storage).
 thread_local std::string t_msg;
@@ -1110,6 +1300,10 @@ void ntc_delete_batch(ntc_batch_t* b) noexcept { delete b; }
 void ntc_encoder_set_batch(ntc_encoder_t* enc, ntc_batch_t* b, ntc_error* error) noexcept
 {
   ntcx::guarded([&] { enc->e.set_batch(b ? &b->b : nullptr); }, error);
+}
+void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* b, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { dec->d.set_batch(b ? &b->b : nullptr); }, error);
 }
 void ntc_batch_flush(ntc_batch_t* b, ntc_error* error) noexcept
 {

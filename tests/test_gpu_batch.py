@@ -98,3 +98,78 @@ def test_detach_flushes_and_delete_discards(capi):
     assert batch.pending == 0
     batch.flush()
     assert len(b.packets) > n_before
+
+
+def _lossy_stream(oracle, w, seed, n=200, p_loss=0.2, rate=4, window=24):
+    rng = np.random.default_rng(seed)
+    enc = oracle.Encoder(galois_field_size=w)
+    enc.set_rate(rate)
+    enc.set_window_size(window)
+    for i in range(n):
+        enc.add_data(rng.integers(0, 256, 4 * int(rng.integers(1, 200)), dtype=np.uint8).tobytes())
+    pkts = [p for p in enc.packets if rng.random() >= p_loss]
+    for i in range(0, len(pkts) - 3, 5):       # local reordering
+        if rng.random() < 0.3:
+            pkts[i], pkts[i + 2] = pkts[i + 2], pkts[i]
+    return pkts
+
+
+@pytest.mark.parametrize("w,in_order,seed", [(8, True, 1), (8, False, 2), (16, True, 3), (4, False, 4),
+                                             (32, True, 12)])
+def test_batched_decoders_match_unbatched(capi, oracle, w, in_order, seed):
+    """Deferred (symbolic) decoding: deliveries, acks and counters equal the immediate decoder's and
+    the oracle's; the state (counters) advances before the flush, the callbacks at the flush."""
+    pkts = _lossy_stream(oracle, w, seed)
+    rng = np.random.default_rng(seed + 100)
+    batch = capi.Batch()
+    a, b = capi.Decoder(w, in_order=in_order), capi.Decoder(w, in_order=in_order)
+    o = oracle.Decoder(in_order=in_order, galois_field_size=w)
+    for d in (a, b, o):
+        d.set_ack_period_ms(0)
+        d.set_ack_nb_packets(20)
+    a.set_batch(batch)
+    for i, p in enumerate(pkts):
+        for d in (a, b, o):
+            d.add_packet(p)
+        for c in capi.Decoder.COUNTERS:
+            assert getattr(a, c) == getattr(b, c), c
+        if rng.random() < 0.1:
+            batch.flush()
+            assert a.data == b.data and a.packets == b.packets
+    batch.flush()
+    assert a.data == b.data == [d for _, d in o.data]
+    assert a.packets == b.packets == o.packets
+    assert b.nb_decoded > 0
+
+
+def test_batch_switching_and_shared_batch(capi, oracle):
+    """Encoders and decoders on one batch; a decoder leaves batch mode mid-stream (its symbols are
+    materialised) and keeps decoding identically."""
+    batch = capi.Batch()
+    rng = np.random.default_rng(9)
+    ea, eb = capi.Encoder(), capi.Encoder()
+    for e in (ea, eb):
+        e.set_rate(3)
+        e.set_window_size(16)
+    ea.set_batch(batch)
+    da, db = capi.Decoder(in_order=True), capi.Decoder(in_order=True)
+    for d in (da, db):
+        d.set_ack_period_ms(0)
+    da.set_batch(batch)
+    sent = 0
+    for step in range(150):
+        data = rng.integers(0, 256, int(rng.integers(1, 600)), dtype=np.uint8).tobytes()
+        ea.add_data(data)
+        eb.add_data(data)
+        batch.flush()                      # ea's packets appear; da's deliveries for older ones
+        assert ea.packets == eb.packets
+        for p in eb.packets[sent:]:
+            if rng.random() >= 0.2:
+                da.add_packet(p)
+                db.add_packet(p)
+        sent = len(eb.packets)
+        if step == 90:
+            da.set_batch(None)             # flush + materialise; immediate from here on
+    batch.flush()
+    assert da.data == db.data and da.packets == db.packets
+    assert db.nb_decoded > 0

@@ -1,7 +1,8 @@
 """Per-packet C ABI (libntc.so) throughput with and without the online batching adaptor: F flows
 (encoders) x M data items of S bytes, window W, rate R (a repair every R sources); the batched
 run attaches every encoder to one ntc_batch_t and flushes once per round (one item per flow).
-Prints one JSON line: packets/s and repairs/s of both runs (wall clock, host + PCIe + GPU).
+The receive side feeds each flow's packets, with 10 % i.i.d. loss, to F decoders the same way.
+Prints one JSON line: packets/s of both runs on both sides (wall clock, host + PCIe + GPU).
 
 usage: python tools/bench_batch.py [--flows 256] [--items 32] [--size 1024] [--window 32] [--rate 4]
 """
@@ -39,6 +40,31 @@ def run(capi, a, batched, data):
             "packets": pk, "repairs": rep}, [e.packets for e in encs]
 
 
+def run_dec(capi, batched, streams):
+    batch = capi.Batch() if batched else None
+    decs = []
+    for _ in streams:
+        d = capi.Decoder(in_order=True)
+        d.set_ack_period_ms(0)
+        if batch is not None:
+            d.set_batch(batch)
+        decs.append(d)
+    rounds = max(len(s) for s in streams)
+    t0 = time.perf_counter()
+    for i in range(rounds):
+        for d, s in zip(decs, streams):
+            if i < len(s):
+                d.add_packet(s[i])
+        if batch is not None and i % 4 == 3:
+            batch.flush()
+    if batch is not None:
+        batch.flush()
+    dt = time.perf_counter() - t0
+    npk = sum(len(s) for s in streams)
+    return ({"s": round(dt, 4), "packets_per_s": round(npk / dt, 1),
+             "decoded": sum(d.nb_decoded for d in decs)}, [d.data for d in decs])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--flows", type=int, default=256)
@@ -53,9 +79,14 @@ def main():
     data = [rng.integers(0, 256, a.size, dtype=np.uint8).tobytes() for _ in range(a.items)]
     imm, p_imm = run(capi, a, False, data)
     bat, p_bat = run(capi, a, True, data)
-    print(json.dumps({"workload": vars(a), "immediate": imm, "batched": bat,
-                      "speedup": round(imm["s"] / bat["s"], 2), "identical_packets": p_imm == p_bat}),
-          flush=True)
+    streams = [[p for p in flow if rng.random() >= 0.1] for flow in p_imm]
+    dimm, d_imm = run_dec(capi, False, streams)
+    dbat, d_bat = run_dec(capi, True, streams)
+    print(json.dumps({"workload": vars(a), "encode": {"immediate": imm, "batched": bat,
+                      "speedup": round(imm["s"] / bat["s"], 2), "identical_packets": p_imm == p_bat},
+                      "decode": {"immediate": dimm, "batched": dbat,
+                                 "speedup": round(dimm["s"] / dbat["s"], 2),
+                                 "identical_deliveries": d_imm == d_bat}}), flush=True)
 
 
 if __name__ == "__main__":

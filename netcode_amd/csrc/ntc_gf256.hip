@@ -422,7 +422,10 @@ __global__ __launch_bounds__(256) void bj_offsets(const uint8_t* __restrict__ co
 // chain iterations without holding VGPRs.  A lane owns two 16-byte pieces of the 2 KiB column
 // span -- bytes [16*lane, +16) and [1024 + 16*lane, +16) -- so each DMA and each store is one
 // contiguous KiB per wave, and a half is valid whenever its 16 bytes lie inside the stride.
-constexpr int kBjRing = 4;
+#ifndef NTC_BJ_RING
+#define NTC_BJ_RING 4
+#endif
+constexpr int kBjRing = NTC_BJ_RING;    // tuning builds: -DNTC_BJ_RING=5
 constexpr uint32_t kBjSlot = 2048;
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p)

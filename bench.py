@@ -8,9 +8,10 @@ HBM.  value = G*k*S payload bytes per step / step time (GiB/s), aggregated over 
 Multi-GPU (torchrun): every rank owns G independent generations with its own id range (weak
 scaling, no data-path collective); only a barrier and a max-reduce of the timing use RCCL.
 
-Extras in the JSON line: roofline (dominant kernel, HIP-event timed on the engine's stream),
-cpu_baseline (the oracle's AVX2 split-nibble path on this host, bounded sample), host-resident
-rate (pinned H2D + kernels + D2H), per-kernel times.
+Extras in the JSON line: roofline (the dominant region-MAC kernel alone, timed by HIP events the
+engine records around its launch on the launch stream -- ntc_gf256_set_timing), an HBM copy probe
+of this device, cpu_baseline (the oracle's AVX2 split-nibble path on this host, bounded sample),
+host-resident rate (pinned H2D + kernels + D2H), per-kernel times.
 """
 from __future__ import annotations
 
@@ -102,11 +103,15 @@ class Workload:
         s = torch.cuda.current_stream(self.dev)
         h = self.enc.engine.handle
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        t_enc, t_plan, t_apply = [], [], []
+        t_enc, t_plan, t_apply, t_emac, t_dmac = [], [], [], [], []
+        _native.check(L.ntc_gf256_set_timing(h, 1), "timing")
+        ms = _native.C.c_float()
         for _ in range(reps):
             ev[0].record(s)
             self.out = self.enc(self.src, self.src_len, self.sid, self.rid, self.out)
             ev[1].record(s)
+            _native.check(L.ntc_gf256_mac_time(h, 0, _native.C.byref(ms)), "mac time")
+            t_emac.append(ms.value)
             _native.check(L.ntc_gf256_decode_plan(
                 h, self.G, self.k, self.r, self.rx_len.data_ptr(), self.smask.data_ptr(),
                 self.out.encoded_size.data_ptr(), self.rmask.data_ptr(), self.sid.data_ptr(),
@@ -117,10 +122,14 @@ class Workload:
                                                    s.cuda_stream), "apply")
             ev[3].record(s)
             torch.cuda.synchronize(self.dev)
+            _native.check(L.ntc_gf256_mac_time(h, 1, _native.C.byref(ms)), "mac time")
+            t_dmac.append(ms.value)
             t_enc.append(ev[0].elapsed_time(ev[1]))
             t_plan.append(ev[1].elapsed_time(ev[2]))
             t_apply.append(ev[2].elapsed_time(ev[3]))
-        return float(np.mean(t_enc)), float(np.mean(t_plan)), float(np.mean(t_apply))
+        _native.check(L.ntc_gf256_set_timing(h, 0), "timing")
+        return (float(np.mean(t_enc)), float(np.mean(t_plan)), float(np.mean(t_apply)),
+                float(np.mean(t_emac)), float(np.mean(t_dmac)))
 
     def verify(self):
         from netcode_amd import status_to_numpy
@@ -173,11 +182,30 @@ class DenseWorkload:
             t_dec.append(ev[2].elapsed_time(ev[3]))
         ti = float(np.mean(t_inv))
         # decode = inversion + MAC with the inverse; report the MAC share as the apply time
-        return float(np.mean(t_enc)), ti, max(float(np.mean(t_dec)) - ti, 1e-6)
+        te, td = float(np.mean(t_enc)), max(float(np.mean(t_dec)) - ti, 1e-6)
+        return te, ti, td, te, td
 
     def verify(self):
         good = bool((self.ok != 0).all().item()) and bool(torch.equal(self.out, self.src))
         return good, int((self.ok != 0).sum().item())
+
+
+def hbm_copy_probe(dev, nbytes=1 << 30, reps=5):
+    """Device-to-device copy bandwidth (read + write bytes / time), GB/s: confirms the HBM peak
+    the roofline divides by on this very device."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    s = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(s)
+    for _ in range(reps):
+        b.copy_(a)
+    ev[1].record(s)
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    del a, b
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
 
 
 def host_rate(w, reps=3):
@@ -302,7 +330,7 @@ def main():
         from netcode_amd.shard import max_over_ranks
         elapsed = max_over_ranks(elapsed, dist, dev)
 
-    t_enc, t_plan, t_apply = w.kernel_times()
+    t_enc, t_plan, t_apply, t_emac, t_dmac = w.kernel_times()
     ms_step = elapsed / a.steps * 1e3
     payload = G * k * S * world
     value = payload / (elapsed / a.steps) / 2**30
@@ -311,10 +339,12 @@ def main():
     enc_bytes = G * (k + r) * S                        # read k*S, write r*S per generation
     m_avg = w.nlost / G
     dec_bytes = G * (k + m_avg) * S                    # read (k-m)*S + m*S, write m*S
-    if t_enc >= t_apply:
-        dom, t_dom, bytes_dom, macs = "encode_mac", t_enc, enc_bytes, G * r * k * S
+    # the MAC kernels alone (engine-recorded HIP events on the launch stream around each MAC
+    # launch -- the same kernels rocprofv3's kernel stats list as gf_mac_bj / gf_mac)
+    if t_emac >= t_dmac:
+        dom, t_dom, bytes_dom, macs = "encode_mac", t_emac, enc_bytes, G * r * k * S
     else:
-        dom, t_dom, bytes_dom, macs = "decode_mac", t_apply, dec_bytes, G * m_avg * k * S
+        dom, t_dom, bytes_dom, macs = "decode_mac", t_dmac, dec_bytes, G * m_avg * k * S
     achieved = bytes_dom / (t_dom * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -336,7 +366,7 @@ def main():
             "kernel_ms": round(t_dom, 4), "algorithmic_bytes_per_launch": int(bytes_dom),
             "byte_macs_per_launch": int(macs),
             "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2),
-            "valu_profile": valu}
+            "valu_profile": valu, "hbm_copy_probe_GBps": hbm_copy_probe(dev)}
 
     line = {"metric": "device-resident GF(256) encode+decode GiB/s, k=128 r=32, 4 KiB pkts, 1/2/4/8 GPU",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
@@ -347,9 +377,9 @@ def main():
                        "m": ("U[0,%d]" % m) if a.mixed else m, "generations_per_gpu": G,
                        "parallelism": f"generation-shard x{world} (no collectives)"},
             "roofline": roof,
-            "kernels_ms": {"encode_mac": round(t_enc, 4),
+            "kernels_ms": {"encode_call": round(t_enc, 4), "encode_mac": round(t_emac, 4),
                            ("dense_invert" if dense else "decode_plan"): round(t_plan, 4),
-                           "decode_mac": round(t_apply, 4)},
+                           "decode_apply_call": round(t_apply, 4), "decode_mac": round(t_dmac, 4)},
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}
     if rank == 0 and world == 1 and not a.no_host_rate:
         line["host_resident_GiBps"] = round(host_rate(w), 3)

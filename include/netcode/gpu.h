@@ -73,6 +73,12 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
 enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2 };
 int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);
 
+/* Profiling: with timing on, the engine records HIP events on the caller's stream around each
+ * region-MAC kernel launch; ntc_gf256_mac_time waits for the last encode (dec = 0) or decode
+ * (dec = 1) MAC and returns that kernel's duration in ms. */
+int  ntc_gf256_set_timing(ntc_gf256_engine* eng, int on);
+int  ntc_gf256_mac_time(ntc_gf256_engine* eng, int dec, float* ms);
+
 /* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture). */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
 

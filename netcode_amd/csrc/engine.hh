@@ -22,6 +22,9 @@ struct ntc_gf256_engine {
   void* joff = nullptr;        // bit-sliced MAC block offsets
   size_t joff_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;
+  // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
+  bool timing = false;
+  hipEvent_t mac_ev[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   // geometry of the last plan (decode_apply must match)
   uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
   // dense-code workspace (ntc_dense.hip): augmented matrices (ping-pong), panel trackers,

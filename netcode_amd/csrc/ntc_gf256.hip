@@ -1167,7 +1167,9 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
   const uint64_t blocks = ((tasks + kWaves - 1) / kWaves + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
+  if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
   hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, st, a);
+  if (e->timing) (void)hipEventRecord(e->mac_ev[dec][1], st);
   return hip_check(hipGetLastError(), what);
 }
 
@@ -1287,7 +1289,34 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->enc_coef);
   (void)hipFree(e->joff);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
+  for (auto& pair : e->mac_ev)
+    for (hipEvent_t ev : pair)
+      if (ev) (void)hipEventDestroy(ev);
   delete e;
+}
+
+int ntc_gf256_set_timing(ntc_gf256_engine* e, int on)
+{
+  if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
+  (void)hipSetDevice(e->device);
+  for (auto& pair : e->mac_ev)
+    for (hipEvent_t& ev : pair)
+      if (!ev) {
+        int rc = hip_check(hipEventCreate(&ev), "hipEventCreate");
+        if (rc) return rc;
+      }
+  e->timing = on != 0;
+  return NTC_GPU_OK;
+}
+
+int ntc_gf256_mac_time(ntc_gf256_engine* e, int dec, float* ms)
+{
+  if (!e || !ms) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (!e->timing) return fail(NTC_GPU_EINVAL, "timing is off (ntc_gf256_set_timing)");
+  hipEvent_t* ev = e->mac_ev[dec ? 1 : 0];
+  int rc = hip_check(hipEventSynchronize(ev[1]), "hipEventSynchronize");
+  if (rc) return rc;
+  return hip_check(hipEventElapsedTime(ms, ev[0], ev[1]), "hipEventElapsedTime");
 }
 
 int ntc_gf256_set_mac_kind(ntc_gf256_engine* e, int kind)

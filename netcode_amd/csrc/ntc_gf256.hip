@@ -677,6 +677,8 @@ struct PrepArgs {
   uint8_t* coef;
   uint16_t* rep_size;
   uint16_t* rep_len;
+  uint32_t* joff;      // non-null: write the bit-sliced MAC's jump offsets (8-row tiles) instead
+  uint32_t ntiles;     //   of the coefficient bytes (bj_offsets fused into the preparation)
 };
 
 __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
@@ -684,23 +686,53 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
   const uint32_t g = blockIdx.x;
   const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
   const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
-  uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp;
-  const uint32_t n = a.k * a.rp;
-  for (uint32_t t = threadIdx.x * 4; t < n; t += 256 * 4) {
-    uint32_t w = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; ++b) {
-      const uint32_t i = (t + b) / a.rp, j = (t + b) % a.rp;
-      if (j < a.r) w |= coefficient(ridb + j, sidb + i) << (8 * b);
+  if (a.joff) {
+    // 4 sites (2 rows x 2 nibbles) per thread and step, like bj_offsets
+    uint4* jo = reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * a.k * a.ntiles * 16u);
+    const uint32_t n4 = a.k * a.ntiles * 4u;
+    for (uint32_t t = threadIdx.x; t < n4; t += 256) {
+      const uint32_t qd = t & 3u, tile = (t >> 2) % a.ntiles, i = (t >> 2) / a.ntiles;
+      const uint32_t j0 = tile * 8u + 2u * qd;
+      const uint32_t c0 = j0 < a.r ? coefficient(ridb + j0, sidb + i) : 0u;
+      const uint32_t c1 = j0 + 1 < a.r ? coefficient(ridb + j0 + 1, sidb + i) : 0u;
+      const uint32_t s0 = 4u * qd * kBjSite;
+      jo[t] = make_uint4(s0 + kBjVo[c0 & 15u], s0 + kBjSite + kBjVo[c0 >> 4],
+                         s0 + 2u * kBjSite + kBjVo[c1 & 15u], s0 + 3u * kBjSite + kBjVo[c1 >> 4]);
     }
-    *reinterpret_cast<uint32_t*>(coef + t) = w;   // rp is a multiple of 4
+  } else {
+    uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp;
+    const uint32_t n = a.k * a.rp;
+    for (uint32_t t = threadIdx.x * 4; t < n; t += 256 * 4) {
+      uint32_t w = 0;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t i = (t + b) / a.rp, j = (t + b) % a.rp;
+        if (j < a.r) w |= coefficient(ridb + j, sidb + i) << (8 * b);
+      }
+      *reinterpret_cast<uint32_t*>(coef + t) = w;   // rp is a multiple of 4
+    }
   }
+  // encoded sizes: the k sources of a repair split over 256 / r thread segments, XOR-reduced
+  __shared__ uint16_t part[256];
   const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
-  for (uint32_t j = threadIdx.x; j < a.r; j += 256) {
+  const uint32_t segs = a.r >= 256 ? 1u : 256u / a.r;
+  for (uint32_t j0 = 0; j0 < a.r; j0 += 256) {
+    const uint32_t rows = min(256u, a.r - j0);
+    const uint32_t sg = rows >= 256 ? 1u : segs;
     uint16_t esz = 0;
-    for (uint32_t i = 0; i < a.k; ++i)
-      esz ^= mul_size(len[i], static_cast<uint8_t>(coefficient(ridb + j, sidb + i)));
-    a.rep_size[static_cast<size_t>(g) * a.r + j] = esz;
+    if (threadIdx.x < rows * sg) {
+      const uint32_t j = j0 + threadIdx.x % rows, seg = threadIdx.x / rows;
+      for (uint32_t i = seg; i < a.k; i += sg)
+        esz ^= mul_size(len[i], static_cast<uint8_t>(coefficient(ridb + j, sidb + i)));
+    }
+    part[threadIdx.x] = esz;
+    __syncthreads();
+    if (threadIdx.x < rows) {
+      uint16_t e = 0;
+      for (uint32_t q = 0; q < sg; ++q) e ^= part[q * rows + threadIdx.x];
+      a.rep_size[static_cast<size_t>(g) * a.r + j0 + threadIdx.x] = e;
+    }
+    __syncthreads();
   }
   if (a.rep_len && threadIdx.x < 64) {
     uint32_t mx = 0;
@@ -1116,7 +1148,9 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
 }
 
 // Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
-int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what)
+// `offsets_ready`: the bit-sliced jump offsets for 8-row tiles are already in e->joff (encode_prep).
+int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what,
+               bool offsets_ready = false)
 {
   mac_fn fn;
   uint32_t rowtile = 32, span;
@@ -1133,13 +1167,17 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
                   : (dec ? gf_mac_bj<8, true> : gf_mac_bj<8, false>);
     a.ntiles = (a.rows + rt - 1) / rt;
     const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 2u * rt;
-    int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
-    if (rc) return rc;
-    a.joff = static_cast<const uint32_t*>(e->joff);
-    const uint64_t n4 = n / 4;
-    hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n4 + 255) / 256)), dim3(256), 0, st,
-                       a.coef, a.rp, rt, a.ntiles, n4, static_cast<uint32_t*>(e->joff));
-    if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
+    if (offsets_ready && rt == 8) {
+      a.joff = static_cast<const uint32_t*>(e->joff);
+    } else {
+      int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
+      if (rc) return rc;
+      a.joff = static_cast<const uint32_t*>(e->joff);
+      const uint64_t n4 = n / 4;
+      hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n4 + 255) / 256)), dim3(256), 0,
+                         st, a.coef, a.rp, rt, a.ntiles, n4, static_cast<uint32_t*>(e->joff));
+      if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
+    }
   } else {
     const int D = pick_d(a.stride);
     span = 256u * D;
@@ -1348,19 +1386,33 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   if (r == 0) return NTC_GPU_OK;
   (void)hipSetDevice(e->device);
   const uint32_t rp = tile_rp(r);
-  rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
-  if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   PrepArgs p{};
   p.G = G; p.k = k; p.r = r; p.rp = rp; p.src_len = src_len; p.sid_base = sid_base;
-  p.rid_base = rid_base; p.coef = static_cast<uint8_t*>(e->enc_coef); p.rep_size = rep_size;
-  p.rep_len = rep_len;
+  p.rid_base = rid_base; p.rep_size = rep_size; p.rep_len = rep_len;
+  // bit-sliced MAC with 8-row tiles: the preparation writes the jump offsets directly
+  static const bool rows16 = [] {
+    const char* v = std::getenv("NTC_GF256_BJ_ROWS");
+    return v && std::atoi(v) == 16;
+  }();
+  const bool fused = use_bitslice(e, stride) && !rows16;
+  if (fused) {
+    p.ntiles = (r + 7u) / 8u;
+    const size_t n = static_cast<size_t>(G) * k * p.ntiles * 16u;
+    rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
+    if (rc) return rc;
+    p.joff = static_cast<uint32_t*>(e->joff);
+  } else {
+    rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+    if (rc) return rc;
+    p.coef = static_cast<uint8_t*>(e->enc_coef);
+  }
   hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
   if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
   a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
-  return launch_mac(e, false, a, st, "encode_mac launch");
+  return launch_mac(e, false, a, st, "encode_mac launch", fused);
 }
 
 int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,

@@ -19,8 +19,11 @@ struct ntc_gf256_engine {
   uint8_t* plan_coef = nullptr;
   void* enc_coef = nullptr;
   size_t enc_coef_cap = 0;
-  void* joff = nullptr;        // bit-sliced MAC block offsets
+  void* joff = nullptr;        // bit-sliced MAC block offsets (encode; decode via bj_offsets)
   size_t joff_cap = 0;
+  void* joff_dec = nullptr;    // decode offsets written by decode_plan (ntc_gf256_decode_batch)
+  size_t joff_dec_cap = 0;
+  bool last_plan_offsets = false;
   int mac_kind = NTC_GF256_MAC_AUTO;
   // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
   bool timing = false;

@@ -768,7 +768,18 @@ struct PlanArgs {
   uint8_t* plan_coef;
   uint32_t rp;
   uint32_t ablate;   // tuning only: bit0 skip elimination, bit1 skip D for received sources
+  uint32_t* joff;    // non-null: also write the bit-sliced MAC's jump offsets (8-row tiles)
+  uint32_t ntiles;
 };
+
+// Jump offsets of one (input position, 8-row tile, 2-row quad) from the two rows' coefficients
+// (the layout bj_offsets writes).
+__device__ __forceinline__ uint4 bj_quad(uint32_t qd, uint32_t c0, uint32_t c1)
+{
+  const uint32_t s0 = 4u * qd * kBjSite;
+  return make_uint4(s0 + kBjVo[c0 & 15u], s0 + kBjSite + kBjVo[c0 >> 4],
+                    s0 + 2u * kBjSite + kBjVo[c1 & 15u], s0 + 3u * kBjSite + kBjVo[c1 >> 4]);
+}
 
 // c * x for the four bytes of x with a per-lane coefficient table (v_perm 3/3/2 split).
 __device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
@@ -787,7 +798,7 @@ __device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
 template <int R, int RM>
 __device__ __forceinline__ void plan_dcol(uint32_t m, uint32_t j, uint32_t sidb,
                                           const uint32_t* rq1, const uint32_t (*minvT)[RM / 4],
-                                          uint8_t* dst, uint32_t rp)
+                                          uint8_t* dst, uint32_t rp, uint4* jo, uint32_t ntiles)
 {
   const uint32_t S1 = sidb + j + 1u;
   uint32_t acc[R / 4];
@@ -807,6 +818,17 @@ __device__ __forceinline__ void plan_dcol(uint32_t m, uint32_t j, uint32_t sidb,
   for (int w = 0; w < R / 4; ++w)
     if (4u * w < rp) d[w] = acc[w];
   for (uint32_t t = R; t < rp; t += 4) d[t / 4] = 0;
+  if (jo) {                                            // this position's jump offsets
+#pragma unroll
+    for (int s = 0; s < R; s += 2) {
+      if (static_cast<uint32_t>(s / 8) >= ntiles) break;
+      const uint32_t c0 = (acc[s / 4] >> (8 * (s % 4))) & 0xFFu;
+      const uint32_t c1 = (acc[(s + 1) / 4] >> (8 * ((s + 1) % 4))) & 0xFFu;
+      jo[(s / 8) * 4 + (s % 8) / 2] = bj_quad((s % 8) / 2, c0, c1);
+    }
+    for (uint32_t q = (R / 8) * 4; q < ntiles * 4; ++q) jo[q] = bj_quad(q & 3u, 0u, 0u);
+  }
+  (void)m;
 }
 
 // RM = row bound of this instantiation (r <= RM): sizes LDS and registers to the launch, so
@@ -968,6 +990,14 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         if (lane < a.rp)
           pc[static_cast<size_t>(q) * a.rp + lane] = static_cast<uint8_t>(lane < m ? minv(lane, q) : 0u);
       }
+      uint4* jo = a.joff ? reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * k * a.ntiles * 16u)
+                         : nullptr;
+      if (jo)
+        for (uint32_t idx = lane; idx < m * a.ntiles * 4u; idx += 64) {
+          const uint32_t q = idx / (a.ntiles * 4u), rem = idx % (a.ntiles * 4u);
+          const uint32_t s0 = (rem / 4u) * 8u + 2u * (rem & 3u);
+          jo[idx] = bj_quad(rem & 3u, s0 < m ? minv(s0, q) : 0u, s0 + 1 < m ? minv(s0 + 1, q) : 0u);
+        }
       if (lane < m) {
         rq1[lane] = ridb + reps[lane] + 1u;
         szs[lane] = rszL[reps[lane]];           // becomes the reduced encoded size of repair q
@@ -1018,13 +1048,15 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         if (!(a.ablate & 2u)) {
           for (uint32_t p0 = lane; p0 < cnt; p0 += 64) {
             uint8_t* dst = pc + static_cast<size_t>(pos_base + p0) * a.rp;
+            uint4* jp = jo ? jo + static_cast<size_t>(pos_base + p0) * a.ntiles * 4u : nullptr;
             const uint32_t j = rl[p0];
-            if (R == 8 || RM == 8) plan_dcol<8, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+            const uint32_t nt = a.ntiles;
+            if (R == 8 || RM == 8) plan_dcol<8, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
             else if constexpr (RM >= 16) {
-              if (R == 16 || RM == 16) plan_dcol<16, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+              if (R == 16 || RM == 16) plan_dcol<16, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
               else if constexpr (RM >= 32) {
-                if (R == 32 || RM == 32) plan_dcol<32, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
-                else if constexpr (RM >= 64) plan_dcol<64, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+                if (R == 32 || RM == 32) plan_dcol<32, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
+                else if constexpr (RM >= 64) plan_dcol<64, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
               }
             }
           }
@@ -1168,7 +1200,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     a.ntiles = (a.rows + rt - 1) / rt;
     const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 2u * rt;
     if (offsets_ready && rt == 8) {
-      a.joff = static_cast<const uint32_t*>(e->joff);
+      // a.joff was set by the caller (encode_prep / decode_plan wrote it)
     } else {
       int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
       if (rc) return rc;
@@ -1326,6 +1358,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_coef);
   (void)hipFree(e->enc_coef);
   (void)hipFree(e->joff);
+  (void)hipFree(e->joff_dec);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   for (auto& pair : e->mac_ev)
     for (hipEvent_t ev : pair)
@@ -1412,13 +1445,14 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
   a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
+  a.joff = static_cast<const uint32_t*>(e->joff);
   return launch_mac(e, false, a, st, "encode_mac launch", fused);
 }
 
-int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
-                          uint16_t* src_len, const uint8_t* src_mask, const uint16_t* rep_size,
-                          const uint8_t* rep_mask, const uint32_t* sid_base,
-                          const uint32_t* rid_base, ntc_gf256_decode_status* status, void* stream)
+static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, uint16_t* src_len,
+                     const uint8_t* src_mask, const uint16_t* rep_size, const uint8_t* rep_mask,
+                     const uint32_t* sid_base, const uint32_t* rid_base,
+                     ntc_gf256_decode_status* status, void* stream, bool offsets)
 {
   if (!e || !src_len || !src_mask || !rep_size || !rep_mask || !status)
     return fail(NTC_GPU_EINVAL, "NULL argument");
@@ -1434,6 +1468,13 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
   p.rep_mask = rep_mask; p.sid_base = sid_base; p.rid_base = rid_base; p.status = status;
   p.plan_m = e->plan_m; p.plan_in = e->plan_in; p.plan_out = e->plan_out;
   p.plan_coef = e->plan_coef; p.rp = rp;
+  if (offsets && r > 0) {
+    p.ntiles = (r + 7u) / 8u;
+    rc = ensure_buf(&e->joff_dec, &e->joff_dec_cap, static_cast<size_t>(G) * k * p.ntiles * 64u,
+                    "hipMalloc joff_dec");
+    if (rc) return rc;
+    p.joff = static_cast<uint32_t*>(e->joff_dec);
+  }
   static const uint32_t ablate = [] {
     const char* v = std::getenv("NTC_GF256_PLAN_ABLATE");
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
@@ -1442,7 +1483,27 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
   auto* fn = r <= 8 ? decode_plan<8> : r <= 16 ? decode_plan<16> : r <= 32 ? decode_plan<32> : decode_plan<64>;
   hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
+  e->last_plan_offsets = p.joff != nullptr;
   return hip_check(hipGetLastError(), "decode_plan launch");
+}
+
+// The bit-sliced path with 8-row tiles (the tile shape encode_prep / decode_plan write offsets for).
+static bool bitslice_rt8(const ntc_gf256_engine* e, uint32_t stride)
+{
+  static const bool rows16 = [] {
+    const char* v = std::getenv("NTC_GF256_BJ_ROWS");
+    return v && std::atoi(v) == 16;
+  }();
+  return use_bitslice(e, stride) && !rows16;
+}
+
+int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
+                          uint16_t* src_len, const uint8_t* src_mask, const uint16_t* rep_size,
+                          const uint8_t* rep_mask, const uint32_t* sid_base,
+                          const uint32_t* rid_base, ntc_gf256_decode_status* status, void* stream)
+{
+  return plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
+                   stream, false);
 }
 
 int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -1459,7 +1520,9 @@ int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   a.in0 = src; a.in1 = rep; a.out = src;
   a.rows_per_gen = e->plan_m; a.in_idx = e->plan_in; a.out_idx = e->plan_out;
   a.coef = e->plan_coef; a.rp = e->last_rp;
-  return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch");
+  const bool ready = e->last_plan_offsets && bitslice_rt8(e, stride);
+  if (ready) a.joff = static_cast<const uint32_t*>(e->joff_dec);
+  return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch", ready);
 }
 
 int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -1470,8 +1533,9 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
 {
   int rc = check_shape(G, k, r, stride);
   if (rc) return rc;
-  rc = ntc_gf256_decode_plan(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base,
-                             rid_base, status, stream);
+  // the plan also writes the bit-sliced MAC's jump offsets when the apply will use them
+  rc = plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
+                 stream, bitslice_rt8(e, stride));
   if (rc) return rc;
   return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
 }

@@ -298,8 +298,13 @@ def main():
     k, r, S, stride, m, Gdef = CONFIGS[a.config]
     G = a.G or Gdef
 
-    import __graft_entry__
-    __graft_entry__.build()
+    if world == 1:
+        import __graft_entry__
+        __graft_entry__.build()          # no-op when the in-tree libraries are up to date
+    else:
+        # ranks never build concurrently: the in-tree .so files are prebuilt (build())
+        import netcode_amd
+        netcode_amd.load_native()
     dense = a.config == "k1024dense"
     if dense:
         w = DenseWorkload(dev, G, k, S, rank)

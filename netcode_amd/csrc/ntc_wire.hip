@@ -50,6 +50,37 @@ __device__ __forceinline__ uint4 load16_shifted(const uint8_t* p, uint32_t sh, u
                     __builtin_amdgcn_alignbyte(d[3], d[2], b), __builtin_amdgcn_alignbyte(d[4], d[3], b));
 }
 
+// 16 bytes of a slot starting at (possibly negative) byte offset off; bytes outside [0, stride)
+// read as zero.  Two guarded aligned loads, realigned like load16_shifted.
+__device__ __forceinline__ uint4 slot16(const uint8_t* base, int32_t off, uint32_t stride)
+{
+  const int32_t a0 = off & ~15;                        // floor to 16 (two's complement)
+  const uint32_t sh = static_cast<uint32_t>(off - a0);
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const uint4 q0 = (a0 >= 0 && static_cast<uint32_t>(a0) < stride)
+                       ? *reinterpret_cast<const uint4*>(base + a0) : z;
+  const uint4 q1 = (sh != 0 && a0 + 16 >= 0 && static_cast<uint32_t>(a0 + 16) < stride)
+                       ? *reinterpret_cast<const uint4*>(base + a0 + 16) : z;
+  if (sh == 0) return q0;
+  const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  const uint32_t b = sh & 3u;
+  uint32_t d[5];
+  switch (sh >> 2) {
+    case 0: d[0] = w[0]; d[1] = w[1]; d[2] = w[2]; d[3] = w[3]; d[4] = w[4]; break;
+    case 1: d[0] = w[1]; d[1] = w[2]; d[2] = w[3]; d[3] = w[4]; d[4] = w[5]; break;
+    case 2: d[0] = w[2]; d[1] = w[3]; d[2] = w[4]; d[3] = w[5]; d[4] = w[6]; break;
+    default: d[0] = w[3]; d[1] = w[4]; d[2] = w[5]; d[3] = w[6]; d[4] = w[7]; break;
+  }
+  return make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], b), __builtin_amdgcn_alignbyte(d[2], d[1], b),
+                    __builtin_amdgcn_alignbyte(d[3], d[2], b), __builtin_amdgcn_alignbyte(d[4], d[3], b));
+}
+
+__device__ __forceinline__ uint32_t get_byte(const uint4& v, uint32_t i)
+{
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+  return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+}
+
 __device__ __forceinline__ void put_byte(uint4& v, uint32_t i, uint32_t b)
 {
   uint32_t* w = reinterpret_cast<uint32_t*>(&v);
@@ -102,16 +133,14 @@ __global__ __launch_bounds__(kWireThreads) void wire_write_repairs(RepairWireArg
   const uint32_t o1 = 7u + symsz, o2 = o1 + ids_bytes(a.k), o3 = o2 + 4u, total = o3 + symsz;
   const uint8_t* sym = a.rep + static_cast<size_t>(p) * a.stride;
   uint8_t* dst = a.out + static_cast<size_t>(p) * a.pkt_stride;
-  auto byte_at = [&](uint32_t q) -> uint32_t {
+  // non-symbol bytes (header, id list, trailer); symbol bytes come from s1 / s2 below
+  auto meta_byte = [&](uint32_t q) -> uint32_t {
     if (q == 0) return 1u;
     if (q < 5) return (rid >> (8 * (4 - q))) & 0xFFu;
     if (q < 7) return (symsz >> (8 * (6 - q))) & 0xFFu;
-    if (q < o1) return sym[q - 7];
     if (q < o2) return ids_byte(a.k, sidb, q - o1);
     if (q < o2 + 2) return (esz >> (8 * (o2 + 1 - q))) & 0xFFu;
-    if (q < o3) return (symsz >> (8 * (o3 - 1 - q))) & 0xFFu;
-    if (q < total) return sym[q - o3];
-    return 0u;
+    return (symsz >> (8 * (o3 - 1 - q))) & 0xFFu;
   };
   const uint32_t nchunks = (total + 15u) / 16u;
   const uint32_t sh2 = (16u - (o3 & 15u)) & 15u;     // symbol offset of chunk starts in copy 2
@@ -124,9 +153,17 @@ __global__ __launch_bounds__(kWireThreads) void wire_write_repairs(RepairWireArg
     } else if (q0 >= o3 && q0 + 16u <= total) {      // inside symbol copy 2
       const uint32_t off = q0 - o3;
       v = load16_shifted(sym + (off & ~15u), sh2, a.stride - (off & ~15u));
-    } else {
+    } else {                                         // boundary chunk: select byte by byte
+      const uint4 s1 = slot16(sym, static_cast<int32_t>(q0) - 7, a.stride);
+      const uint4 s2 = slot16(sym, static_cast<int32_t>(q0) - static_cast<int32_t>(o3), a.stride);
       v = make_uint4(0, 0, 0, 0);
-      for (uint32_t i = 0; i < 16; ++i) put_byte(v, i, byte_at(q0 + i));
+      for (uint32_t i = 0; i < 16; ++i) {
+        const uint32_t q = q0 + i;
+        const uint32_t x = q >= total ? 0u
+                         : q >= o3 ? get_byte(s2, i)
+                         : (q >= 7 && q < o1) ? get_byte(s1, i) : meta_byte(q);
+        put_byte(v, i, x);
+      }
     }
     *reinterpret_cast<uint4*>(dst + q0) = v;
   }

@@ -610,15 +610,20 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 // One wave per (generation, RT-row tile, 2 KiB column span).  Blocks are renumbered so that each
 // XCD (block b runs on XCD b % 8) owns a contiguous range of tasks: the row tiles of one
 // generation then share that XCD's L2 instead of each pulling the sources from HBM.
+#ifndef NTC_BJ_WPB
+#define NTC_BJ_WPB 4
+#endif
+constexpr int kBjWaves = NTC_BJ_WPB;     // waves (independent tasks) per workgroup; tuning builds
+
 template <int RT, bool DEC, int ABL = 0>
-__global__ __launch_bounds__(256) void gf_mac_bj(MacArgs a)
+__global__ __launch_bounds__(64 * kBjWaves) void gf_mac_bj(MacArgs a)
 {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kWaves * kBjRing * kBjSlot];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kBjWaves * kBjRing * kBjSlot];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t nb = gridDim.x;                       // a multiple of 8 (launch_mac)
   const uint32_t b = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
-  uint32_t task = uniform(b * kWaves + wave);
+  uint32_t task = uniform(b * kBjWaves + wave);
   const uint32_t cc = task % a.ncolchunks;
   task /= a.ncolchunks;
   const uint32_t tile = task % a.nrowchunks;
@@ -1235,10 +1240,11 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   a.nrowchunks = (a.rows + rowtile - 1) / rowtile;
   a.ncolchunks = (a.stride + span - 1) / span;
   const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
-  const uint64_t blocks = ((tasks + kWaves - 1) / kWaves + blk_align - 1) / blk_align * blk_align;
+  const uint64_t wpb = rowtile <= 16 ? kBjWaves : kWaves;     // bit-sliced : v_perm kernel
+  const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
-  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, a);
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][1], st);
   return hip_check(hipGetLastError(), what);
 }

@@ -205,3 +205,34 @@ def test_full_size_round_trip_config3(gpu, oracle):
     _, _, ost = oracle.decode_batch(s16 * mask[:, :, None], l16 * mask, mask, orep, orsz,
                                     np.ones((G, r), np.uint8), threads=16)
     assert (st == ost).all()
+
+
+def test_mac_timing_api(gpu):
+    """ntc_gf256_set_timing / mac_time (the bench's roofline clock): the recorded MAC durations
+    are positive and no longer than the whole encode / decode call around them."""
+    import ctypes as C
+    import torch
+    from netcode_amd import BatchDecoder, BatchEncoder, _native
+    from netcode_amd.engine import Engine
+    G, k, r, S = 64, 64, 16, 4096
+    src, lens = make_sources(G, k, S, S, seed=3)
+    s_t, l_t = dev(src, gpu), dev(lens, gpu)
+    L, h = _native.load(), Engine.get(gpu).handle
+    _native.check(L.ntc_gf256_set_timing(h, 1), "timing")
+    try:
+        s = torch.cuda.current_stream(gpu)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(s)
+        enc = BatchEncoder(k, r, gpu)(s_t, l_t)
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        ms = C.c_float()
+        _native.check(L.ntc_gf256_mac_time(h, 0, C.byref(ms)), "mac time")
+        assert 0 < ms.value <= ev[0].elapsed_time(ev[1]) + 1e-3
+        smask = loss_exact_m(G, k, 8, 4)
+        BatchDecoder(k, r, gpu)(s_t, l_t, dev(smask, gpu), enc.repairs, enc.encoded_size,
+                                torch.ones((G, r), dtype=torch.uint8, device=gpu))
+        _native.check(L.ntc_gf256_mac_time(h, 1, C.byref(ms)), "mac time")
+        assert ms.value > 0
+    finally:
+        _native.check(L.ntc_gf256_set_timing(h, 0), "timing")

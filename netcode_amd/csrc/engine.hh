@@ -24,6 +24,8 @@ struct ntc_gf256_engine {
   void* joff_dec = nullptr;    // decode offsets written by decode_plan (ntc_gf256_decode_batch)
   size_t joff_dec_cap = 0;
   bool last_plan_offsets = false;
+  void* row_ptr = nullptr;     // bit-sliced decode: input row address per plan position
+  size_t row_ptr_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;
   // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
   bool timing = false;

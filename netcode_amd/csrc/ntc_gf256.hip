@@ -165,6 +165,8 @@ struct MacArgs {
   uint32_t rp;
   const uint32_t* joff;        // bit-sliced kernel: block offsets [G][k][ntiles][16]
   uint32_t ntiles;
+  const uint64_t* row_ptr;     // bit-sliced decode: input row address per plan position,
+                               // [G][k + kBjRing] (plan_rows; the tail repeats position k-1)
 };
 
 // ---- hand-scheduled scalar loads -------------------------------------------------------------
@@ -484,31 +486,21 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   const uint32_t x0 = v0 ? c0 : 0u, x1 = v1 ? c1 : 0u;  // invalid pieces read column 0 (unused)
   const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
   const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
-  const uint16_t* in = DEC ? a.in_idx + static_cast<size_t>(g) * k : nullptr;
   const uint32_t jstep = a.ntiles * 2u * RT;
   const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * (2u * RT);
   constexpr int NJ = R == 16 ? 2 : 1;     // u32x16 offset vectors per source
-  // Offsets and plan entries are loaded with ordinary uniform loads through the constant address
-  // space (s_load, waits placed by the compiler).
-  // decode: plan_in entry i via the dword holding it (4-byte aligned scalar load); the shift that
-  // selects the entry is applied at the use, so the load's wait lands one iteration later.
-  auto in_word = [&](uint32_t i) -> uint32_t {
-    const uintptr_t ad = reinterpret_cast<uintptr_t>(in + i);
-    return const_load<uint32_t>(reinterpret_cast<const void*>(ad & ~static_cast<uintptr_t>(3)));
-  };
-  auto in_shift = [&](uint32_t i) -> uint32_t {
-    return 8u * (static_cast<uint32_t>(reinterpret_cast<uintptr_t>(in + i)) & 2u);
-  };
-  auto row_of = [&](uint32_t i, uint32_t w) -> const uint8_t* {
-    if constexpr (DEC) {
-      const uint32_t ii = (w >> in_shift(i)) & 0xFFFFu;
-      return ii < k ? base0 + ii * stride : base1 + (ii - k) * stride;
-    } else {
-      (void)w;
-      return base0 + i * stride;
-    }
-  };
+  // Offsets and row addresses are loaded with ordinary uniform loads through the constant address
+  // space (s_load, waits placed by the compiler).  Decode reads each input row's address from the
+  // plan_rows table (padded by kBjRing entries, so the prefetches past position k-1 need no
+  // clamp); encode advances its row and offset pointers by a conditional add per source.  Both
+  // keep the per-source scalar work to a few instructions.
+  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBjRing) : nullptr;
   auto clampk = [&](uint32_t i) -> uint32_t { return i < k ? i : k - 1; };
+  auto row_at = [&](uint32_t i) -> const uint8_t* {    // prologue only
+    if constexpr (DEC) return reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i));
+    else return base0 + clampk(i) * stride;
+  };
+  (void)base1;
 
   uint32_t acc[R][8];
 #pragma unroll
@@ -521,12 +513,12 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   // read of source i+1 in flight, DMAs of i+2 .. i+kBjRing-1 in flight.
 #pragma unroll
   for (int q = 0; q < kBjRing - 1; ++q) {
-    const uint32_t iq = clampk(q);
-    const uint8_t* row = row_of(iq, DEC ? in_word(iq) : 0u);
+    const uint8_t* row = row_at(q);
     dma_source(row + x0, row + x1, ring + q * kBjSlot);
   }
-  uint32_t wn = 0;
-  if constexpr (DEC) wn = in_word(clampk(kBjRing - 1));
+  // row of source i + kBjRing - 1, the refill of iteration i (decode: loaded one iteration ahead)
+  const uint8_t* nrow = row_at(kBjRing - 1);
+  const uint32_t* jp = jrow;                           // offsets of source min(i + 1, k - 1)
   u32x16 on[NJ];
 #pragma unroll
   for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + 16 * h);
@@ -546,15 +538,15 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     vm_wait<2 * (kBjRing - 3)>();
     ring_read(ring_p + ((i + 1) % kBjRing) * kBjSlot, lane, ycur);
     {   // refill the slot of source i-1 (read and consumed) with source i + kBjRing - 1
-      const uint32_t iq = clampk(i + kBjRing - 1);
-      const uint8_t* row = row_of(iq, wn);
-      dma_source(row + x0, row + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
-      if constexpr (DEC) wn = in_word(clampk(i + kBjRing));
+      dma_source(nrow + x0, nrow + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
+      if constexpr (DEC)
+        nrow = reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i + kBjRing));
+      else
+        nrow += (i + kBjRing < k) ? stride : 0u;
     }
-    const uint32_t i1 = clampk(i + 1);
+    if constexpr (!(ABL & 16)) jp += (i + 1 < k) ? jstep : 0u;
 #pragma unroll
-    for (int h = 0; h < NJ; ++h)
-      on[h] = const_load<u32x16>(jrow + static_cast<size_t>((ABL & 16) ? 0u : i1) * jstep + 16 * h);
+    for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jp + 16 * h);
     if constexpr (!(ABL & 2)) {
       NTC_BJ_TABLES(Y)
     } else {
@@ -643,6 +635,27 @@ __global__ __launch_bounds__(64 * kBjWaves) void gf_mac_bj(MacArgs a)
   }
   if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
   else mac_tile_bj<4, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
+}
+
+// Input row address of every plan position for the bit-sliced decode MAC: position i < k reads
+// received source slot plan_in[i] (< k) or repair plan_in[i] - k; entries k .. k + kBjRing - 1
+// repeat position k - 1 (the MAC's ring prefetches run past the last source).  Generations with
+// nothing to decode are skipped (the MAC does not read them).
+__global__ __launch_bounds__(256) void plan_rows(const uint16_t* __restrict__ plan_m,
+                                                 const uint16_t* __restrict__ plan_in, uint32_t G,
+                                                 uint32_t k, uint32_t r, uint64_t stride,
+                                                 const uint8_t* src, const uint8_t* rep,
+                                                 uint64_t* __restrict__ rows)
+{
+  const uint32_t kp = k + kBjRing;
+  const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (idx >= static_cast<uint64_t>(G) * kp) return;
+  const uint32_t g = static_cast<uint32_t>(idx / kp), i = static_cast<uint32_t>(idx % kp);
+  if (plan_m[g] == 0) return;
+  const uint32_t ii = plan_in[static_cast<size_t>(g) * k + (i < k ? i : k - 1)];
+  const uint8_t* row = ii < k ? src + (static_cast<uint64_t>(g) * k + ii) * stride
+                              : rep + (static_cast<uint64_t>(g) * r + (ii - k)) * stride;
+  rows[idx] = reinterpret_cast<uint64_t>(row);
 }
 
 // Encode (DEC = false): rep[g][rows] = C_g * src[g]; decode (DEC = true): the plan's D_g applied to
@@ -1203,6 +1216,16 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     fn = rt == 16 ? (dec ? gf_mac_bj<16, true> : gf_mac_bj<16, false>)
                   : (dec ? gf_mac_bj<8, true> : gf_mac_bj<8, false>);
     a.ntiles = (a.rows + rt - 1) / rt;
+    if (dec) {   // input row addresses of the plan positions (MacArgs::row_ptr)
+      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
+      int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
+      if (rc) return rc;
+      hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
+                         a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
+                         a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
+      if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
+      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
+    }
     const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 2u * rt;
     if (offsets_ready && rt == 8) {
       // a.joff was set by the caller (encode_prep / decode_plan wrote it)
@@ -1365,6 +1388,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->enc_coef);
   (void)hipFree(e->joff);
   (void)hipFree(e->joff_dec);
+  (void)hipFree(e->row_ptr);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   for (auto& pair : e->mac_ev)
     for (hipEvent_t ev : pair)

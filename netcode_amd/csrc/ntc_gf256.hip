@@ -522,6 +522,11 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   u32x16 on[NJ];
 #pragma unroll
   for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + 16 * h);
+  auto next_offsets = [&](uint32_t i) {
+    if constexpr (!(ABL & 16)) jp += (i + 1 < k) ? jstep : 0u;
+#pragma unroll
+    for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jp + 16 * h);
+  };
   uint32_t ycur[8];
   vm_wait<2 * (kBjRing - 2)>();
   ring_read(ring_p, lane, ycur);
@@ -544,9 +549,9 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
       else
         nrow += (i + kBjRing < k) ? stride : 0u;
     }
-    if constexpr (!(ABL & 16)) jp += (i + 1 < k) ? jstep : 0u;
-#pragma unroll
-    for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jp + 16 * h);
+    // offsets of source i+1, loaded before the chain so their latency hides behind it (loading
+    // them after the chain into the same registers saves the copies but measured 10 % slower)
+    next_offsets(i);
     if constexpr (!(ABL & 2)) {
       NTC_BJ_TABLES(Y)
     } else {
@@ -1101,6 +1106,308 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   }
 }
 
+// ------------------------------------------------------------- decode plan, r <= 32 (v2) ----
+// Register-resident decode_plan for r <= 32 (config 3 and every shape with at most 32 repairs):
+// one wave per generation, four generations per block sharing one LDS copy of the v_perm tables.
+// Column layout: lane c < 2m holds column c of the augmented matrix [M | I] in W = RM/4 dwords
+// (rows packed four per dword), so a Gauss-Jordan step is a rank-1 update of every lane's own
+// registers: F = column p (v_readlane broadcast), y_c = A[p][c] / piv (one mul4 with the
+// inverse's table), A[:, c] ^= F' * y_c with F'[p] = F[p] ^ 1, which leaves row p = y and clears
+// column p elsewhere.  A zero on the diagonal (rare) swaps in the first nonzero row below it, as
+// jerasure does (invert_matrix.cc:49-60); rank and M^-1 do not depend on the pivot order anyway.
+// The decoded sizes use the same columns: dec_size[s] = sum_q Minv[s][q] (x) rsz_q ^ sum_j D[s][j]
+// (x) len_j (decoder.cc:402-404, 484-497, linear in the bytes of each u16), each lane
+// accumulating the terms of the columns it owns, then one XOR butterfly across the wave.
+constexpr int kPlanWaves = 4;
+
+__constant__ __attribute__((aligned(16))) PermTables d_pinv = make_inv_perm_tables();
+
+template <int W>
+__device__ __forceinline__ uint32_t byte_dyn(const uint32_t (&v)[W], uint32_t i)
+{
+  uint32_t x = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) x = (static_cast<uint32_t>(w) == (i >> 2)) ? v[w] : x;
+  return (x >> (8u * (i & 3u))) & 0xFFu;
+}
+
+template <int W>
+__device__ __forceinline__ void set_byte_dyn(uint32_t (&v)[W], uint32_t i, uint32_t b)
+{
+  const uint32_t sh = 8u * (i & 3u);
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (static_cast<uint32_t>(w) == (i >> 2)) v[w] = (v[w] & ~(0xFFu << sh)) | (b << sh);
+}
+
+// Gauss-Jordan step for column P (compile-time, so every register index is static): false when
+// column P has no nonzero at or below row P (M singular).
+template <int W, int P>
+__device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const uint32_t (*ptab)[8])
+{
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  constexpr int pw = P >> 2, ps = 8 * (P & 3);
+  uint32_t F[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) F[w] = __builtin_amdgcn_readlane(col[w], P);
+  uint32_t piv = (F[pw] >> ps) & 0xFFu;
+  if (piv == 0) {
+    // first row below P with a nonzero in column P (rows >= m are zero)
+    uint32_t q = kNone;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t below = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (4 * w + b > P) below |= 0x80u << (8 * b);
+      const uint32_t f = F[w];
+      const uint32_t nz = (((f & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | f) & below;
+      if (q == kNone && nz != 0) q = 4u * w + (__builtin_ctz(nz) >> 3);
+    }
+    if (q == kNone) return false;
+    const uint32_t bp = (col[pw] >> ps) & 0xFFu, bq = byte_dyn<W>(col, q);
+    col[pw] = (col[pw] & ~(0xFFu << ps)) | (bq << ps);
+    set_byte_dyn<W>(col, q, bp);
+#pragma unroll
+    for (int w = 0; w < W; ++w) F[w] = __builtin_amdgcn_readlane(col[w], P);
+    piv = (F[pw] >> ps) & 0xFFu;
+  }
+  const uint32_t* ti = d_pinv.w[piv];
+  const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
+  const uint32_t y = mul4(tinv, (col[pw] >> ps) & 0xFFu);    // A[P][c] / piv
+  const uint4 ab = *reinterpret_cast<const uint4*>(&ptab[y][0]);
+  const uint32_t ty[5] = {ab.x, ab.y, ab.z, ab.w, ptab[y][4]};
+  F[pw] ^= 1u << ps;
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (4u * w < m) col[w] ^= mul4(ty, F[w]);
+  return true;
+}
+
+template <int W, int P, int RM>
+__device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], uint32_t m, const uint32_t (*ptab)[8])
+{
+  if constexpr (P == RM) {
+    return true;
+  } else {
+    if (static_cast<uint32_t>(P) >= m) return true;
+    if (!gj_step<W, P>(col, m, ptab)) return false;
+    return gj_pivots<W, P + 1, RM>(col, m, ptab);
+  }
+}
+
+template <int RM>
+__global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
+{
+  static_assert(RM == 8 || RM == 16 || RM == 32, "the column layout needs 2 * RM <= 64 lanes");
+  constexpr int W = RM / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
+  __shared__ uint16_t s_miss[kPlanWaves][RM];
+  __shared__ uint16_t s_recv[kPlanWaves][RM];
+  __shared__ __attribute__((aligned(16))) uint32_t s_minvT[kPlanWaves][RM][W];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
+    for (uint32_t i = threadIdx.x; i < 512u; i += 64u * kPlanWaves) dst[i] = src[i];
+  }
+  __syncthreads();   // the only block-wide barrier: the waves below are independent generations
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = uniform(threadIdx.x >> 6);
+  const uint32_t g = blockIdx.x * kPlanWaves + wv;
+  if (g >= a.G) return;
+  uint16_t* miss = s_miss[wv];
+  uint16_t* recv = s_recv[wv];
+  uint32_t (*minvT)[W] = s_minvT[wv];
+  auto wave_sync = [] {    // LDS written by some lanes, read by others of the same wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto tab = [&](uint32_t c, uint32_t (&t)[5]) {
+    const uint4 ab = *reinterpret_cast<const uint4*>(&ptab[c][0]);
+    t[0] = ab.x; t[1] = ab.y; t[2] = ab.z; t[3] = ab.w; t[4] = ptab[c][4];
+  };
+
+  const uint32_t k = a.k, r = a.r;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
+  const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
+  const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+
+  uint32_t m = 0;
+  for (uint32_t base = 0; base < k; base += 64) {
+    const uint32_t idx = base + lane;
+    const bool lost = idx < k && smask[idx] == 0;
+    const uint64_t b = __ballot(lost);
+    if (lost) {
+      const uint32_t pos = m + __popcll(b & lt);
+      if (pos < RM) miss[pos] = static_cast<uint16_t>(idx);
+    }
+    m += __popcll(b);
+  }
+  uint32_t nrecv = 0;
+  {
+    const bool got = lane < r && rmask[lane] != 0;      // r <= RM <= 32
+    const uint64_t b = __ballot(got);
+    if (got) recv[__popcll(b & lt)] = static_cast<uint16_t>(lane);
+    nrecv = __popcll(b);
+  }
+  wave_sync();
+
+  ntc_gf256_decode_status st{};
+  st.nb_missing = static_cast<uint16_t>(m);
+  st.last_repair = 0xFFFF;
+  uint32_t mm = 0;
+  if (m == 0) {
+    st.state = 1;
+    st.nb_useless = static_cast<uint16_t>(nrecv);
+  } else if (nrecv < m || m > static_cast<uint32_t>(RM)) {
+    st.state = 2;
+  } else {
+    // lane q < nrecv: R1 of the q-th received repair; lane c < m: S1 of missing source c
+    const uint32_t rid1 = lane < nrecv ? ridb + recv[lane] + 1u : 0u;
+    const uint32_t S1 = lane < m ? sidb + miss[lane] + 1u : 0u;
+    auto coef = [&](uint32_t R1) -> uint32_t {      // galois_field.hh:143-158
+      return lane < m ? ((R1 + S1) * R1) % 255u + 1u : 0u;
+    };
+    // rows 0 .. m-2: the first m-1 received repairs; identity block in lanes m .. 2m-1
+    uint32_t orig[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t q = 4u * w + b;
+        if (q + 1 < m) v |= coef(__builtin_amdgcn_readlane(rid1, q)) << (8 * b);
+      }
+      if (lane >= m && lane < 2 * m && ((lane - m) >> 2) == static_cast<uint32_t>(w))
+        v |= 1u << (8u * ((lane - m) & 3u));
+      orig[w] = v;
+    }
+    uint32_t col[W];
+    bool ok = false;
+    uint32_t t = m - 1;
+    for (; t < nrecv; ++t) {
+      // row m-1: received repair t (decoder.cc:448-468 retries with each newer repair)
+      const uint32_t ct = coef(__builtin_amdgcn_readlane(rid1, t));
+#pragma unroll
+      for (int w = 0; w < W; ++w) col[w] = orig[w];
+      set_byte_dyn<W>(col, m - 1, ct | byte_dyn<W>(orig, m - 1));
+      if (gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
+    }
+    if (!ok) {
+      st.state = 3;
+      const uint32_t f = nrecv - m + 1;
+      st.nb_failed = static_cast<uint8_t>(f > 255 ? 255 : f);
+    } else {
+      st.state = 0;
+      const uint32_t f = t - (m - 1);
+      st.nb_failed = static_cast<uint8_t>(f > 255 ? 255 : f);
+      st.nb_decoded = static_cast<uint16_t>(m);
+      st.nb_useless = static_cast<uint16_t>(nrecv - 1 - t);
+      st.last_repair = recv[t];
+      mm = m;
+      const uint32_t rp = a.rp, ntiles = a.ntiles;
+      uint16_t* pin = a.plan_in + static_cast<size_t>(g) * k;
+      uint8_t* pc = a.plan_coef + static_cast<size_t>(g) * k * rp;
+      uint16_t* pout = a.plan_out + static_cast<size_t>(g) * rp;
+      uint16_t* slen = a.src_len + static_cast<size_t>(g) * k;
+      uint4* jo0 = a.joff ? reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * k * ntiles * 16u)
+                          : nullptr;
+      // plan row of input position `pos`: the rp coefficient bytes and the MAC's jump offsets
+      auto emit = [&](uint32_t pos, const uint32_t (&v)[W]) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(pc + static_cast<size_t>(pos) * rp);
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (4u * w < rp) d[w] = v[w];
+        if (jo0) {
+          uint4* jo = jo0 + static_cast<size_t>(pos) * ntiles * 4u;
+#pragma unroll
+          for (int s = 0; s < RM; s += 2) {
+            if (static_cast<uint32_t>(s / 8) >= ntiles) break;
+            const uint32_t c0 = (v[s / 4] >> (8 * (s % 4))) & 0xFFu;
+            const uint32_t c1 = (v[(s + 1) / 4] >> (8 * ((s + 1) % 4))) & 0xFFu;
+            jo[(s / 8) * 4 + (s % 8) / 2] = bj_quad((s % 8) / 2, c0, c1);
+          }
+        }
+      };
+      uint32_t LO[W], HI[W];     // this lane's decoded-size terms, low and high length bytes
+#pragma unroll
+      for (int w = 0; w < W; ++w) LO[w] = HI[w] = 0;
+      auto size_terms = [&](uint32_t len, const uint32_t (&v)[W]) {
+        uint32_t tl[5], th[5];
+        tab(len & 0xFFu, tl);
+        tab(len >> 8, th);
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (4u * w < m) {
+            LO[w] ^= mul4(tl, v[w]);
+            HI[w] ^= mul4(th, v[w]);
+          }
+      };
+      // R1 of the repair in row q (rows 0 .. m-2: received repairs 0 .. m-2; row m-1: repair t)
+      const uint32_t t_rid1 = __builtin_amdgcn_readlane(rid1, t);
+      const uint32_t row_r1 = (lane == m - 1) ? t_rid1 : rid1;
+      // Positions 0 .. m-1: the chosen repairs, D[s][q] = Minv[s][q] = column m + q
+      if (lane >= m && lane < 2 * m) {
+        const uint32_t q = lane - m;
+        const uint32_t rq = (q + 1 < m) ? recv[q] : recv[t];
+        pin[q] = static_cast<uint16_t>(k + rq);
+        emit(q, col);
+#pragma unroll
+        for (int w = 0; w < W; ++w) minvT[q][w] = col[w];
+        size_terms(a.rep_size[static_cast<size_t>(g) * r + rq], col);
+      }
+      if (lane < rp) pout[lane] = lane < m ? miss[lane] : 0;
+      wave_sync();
+      // Positions m .. k-1: received sources ascending, D[s][j] = sum_q Minv[s][q] * c(q, j)
+      uint32_t pos_base = m;
+      for (uint32_t base = 0; base < k; base += 64) {
+        const uint32_t j = base + lane;
+        const bool got = j < k && smask[j] != 0;
+        const uint64_t b = __ballot(got);
+        if (got) {
+          const uint32_t pos = pos_base + __popcll(b & lt);
+          pin[pos] = static_cast<uint16_t>(j);
+          const uint32_t Sj = sidb + j + 1u;
+          uint32_t acc[W];
+#pragma unroll
+          for (int w = 0; w < W; ++w) acc[w] = 0;
+          for (uint32_t q = 0; q < m; ++q) {
+            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q);
+            uint32_t tc[5];
+            tab(((R1 + Sj) * R1) % 255u + 1u, tc);
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+              if (4u * w < m) acc[w] ^= mul4(tc, minvT[q][w]);
+          }
+          emit(pos, acc);
+          size_terms(slen[j], acc);
+        }
+        pos_base += __popcll(b);
+      }
+      // XOR-reduce the size terms over the wave; lane s < m keeps byte s
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (4u * w < m) {
+            LO[w] ^= __shfl_xor(LO[w], off);
+            HI[w] ^= __shfl_xor(HI[w], off);
+          }
+      if (lane < m) {
+        const uint32_t lo = byte_dyn<W>(LO, lane), hi = byte_dyn<W>(HI, lane);
+        slen[miss[lane]] = static_cast<uint16_t>(lo | (hi << 8));
+      }
+    }
+  }
+  if (lane == 0) {
+    a.plan_m[g] = static_cast<uint16_t>(mm);
+    a.status[g] = st;
+  }
+}
+
 // ----------------------------------------------------------------------- region multiply ----
 __global__ __launch_bounds__(256) void region_mul(const uint8_t* __restrict__ src,
                                                   uint8_t* __restrict__ dst, size_t len,
@@ -1510,8 +1817,20 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
   p.ablate = ablate;
-  auto* fn = r <= 8 ? decode_plan<8> : r <= 16 ? decode_plan<16> : r <= 32 ? decode_plan<32> : decode_plan<64>;
-  hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
+  // r <= 32: the register-resident plan (four generations per block); NTC_GF256_PLAN=lds selects
+  // the LDS Gauss-Jordan kernel instead (A/B only; r > 32 always uses it)
+  static const bool lds_plan = [] {
+    const char* v = std::getenv("NTC_GF256_PLAN");
+    return v && !std::strcmp(v, "lds");
+  }();
+  if (r <= 32 && !lds_plan && !ablate) {
+    auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;
+    hipLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,
+                       static_cast<hipStream_t>(stream), p);
+  } else {
+    auto* fn = r <= 8 ? decode_plan<8> : r <= 16 ? decode_plan<16> : r <= 32 ? decode_plan<32> : decode_plan<64>;
+    hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
+  }
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
   e->last_plan_offsets = p.joff != nullptr;
   return hip_check(hipGetLastError(), "decode_plan launch");

@@ -692,6 +692,14 @@ __global__ __launch_bounds__(256) void gf_mac(MacArgs a)
 // (galois_field.hh:143-158, uint32 wraparound) as [k][rp] bytes, the encoded sizes
 // (detail/encoder.cc:38, 61-62: XOR of bytewise-coded u16 lengths) and the repair symbol length
 // (max source length, detail/encoder.cc:26, 44-48).
+// c * x for the four bytes of x with a per-lane coefficient table (v_perm 3/3/2 split).
+__device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
+{
+  return __builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u) ^
+         __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
+         __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
+}
+
 struct PrepArgs {
   uint32_t G, k, r, rp;
   const uint16_t* src_len;
@@ -709,6 +717,17 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
   const uint32_t g = blockIdx.x;
   const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
   const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
+  // LDS copies of the v_perm tables (encoded sizes) and of the block offsets (jump offsets):
+  // per-lane lookups that would otherwise be dependent global loads
+  __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
+  __shared__ uint32_t vo[16];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
+    for (uint32_t i = threadIdx.x; i < 512u; i += 256u) dst[i] = src[i];
+    if (threadIdx.x < 16) vo[threadIdx.x] = kBjVo[threadIdx.x];
+  }
+  __syncthreads();
   if (a.joff) {
     // 4 sites (2 rows x 2 nibbles) per thread and step, like bj_offsets
     uint4* jo = reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * a.k * a.ntiles * 16u);
@@ -719,8 +738,8 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
       const uint32_t c0 = j0 < a.r ? coefficient(ridb + j0, sidb + i) : 0u;
       const uint32_t c1 = j0 + 1 < a.r ? coefficient(ridb + j0 + 1, sidb + i) : 0u;
       const uint32_t s0 = 4u * qd * kBjSite;
-      jo[t] = make_uint4(s0 + kBjVo[c0 & 15u], s0 + kBjSite + kBjVo[c0 >> 4],
-                         s0 + 2u * kBjSite + kBjVo[c1 & 15u], s0 + 3u * kBjSite + kBjVo[c1 >> 4]);
+      jo[t] = make_uint4(s0 + vo[c0 & 15u], s0 + kBjSite + vo[c0 >> 4],
+                         s0 + 2u * kBjSite + vo[c1 & 15u], s0 + 3u * kBjSite + vo[c1 >> 4]);
     }
   } else {
     uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp;
@@ -745,8 +764,10 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
     uint16_t esz = 0;
     if (threadIdx.x < rows * sg) {
       const uint32_t j = j0 + threadIdx.x % rows, seg = threadIdx.x / rows;
+      // both length bytes times c in one v_perm lookup (galois_field.hh:108-115 codes a u16 as
+      // a 2-byte region; a zero length stays zero)
       for (uint32_t i = seg; i < a.k; i += sg)
-        esz ^= mul_size(len[i], static_cast<uint8_t>(coefficient(ridb + j, sidb + i)));
+        esz ^= static_cast<uint16_t>(mul4(ptab[coefficient(ridb + j, sidb + i)], len[i]));
     }
     part[threadIdx.x] = esz;
     __syncthreads();
@@ -804,13 +825,6 @@ __device__ __forceinline__ uint4 bj_quad(uint32_t qd, uint32_t c0, uint32_t c1)
                     s0 + 2u * kBjSite + kBjVo[c1 & 15u], s0 + 3u * kBjSite + kBjVo[c1 >> 4]);
 }
 
-// c * x for the four bytes of x with a per-lane coefficient table (v_perm 3/3/2 split).
-__device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
-{
-  return __builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u) ^
-         __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
-         __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
-}
 
 
 // D column of one received-source position j (one lane): D[s][j] = sum_q (M^-1)[s][q] * c(q, j)
@@ -1204,7 +1218,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
   __shared__ uint16_t s_miss[kPlanWaves][RM];
   __shared__ uint16_t s_recv[kPlanWaves][RM];
-  __shared__ __attribute__((aligned(16))) uint32_t s_minvT[kPlanWaves][RM][W];
+  // M^-1 column q as the three v_perm selector words per dword (bits 0-2, 3-5, 6-7 of each byte)
+  __shared__ __attribute__((aligned(16))) uint32_t s_minvS[kPlanWaves][RM][3][W];
   {
     const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
@@ -1217,7 +1232,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   if (g >= a.G) return;
   uint16_t* miss = s_miss[wv];
   uint16_t* recv = s_recv[wv];
-  uint32_t (*minvT)[W] = s_minvT[wv];
+  uint32_t (*minvS)[3][W] = s_minvS[wv];
   auto wave_sync = [] {    // LDS written by some lanes, read by others of the same wave
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1262,7 +1277,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   if (m == 0) {
     st.state = 1;
     st.nb_useless = static_cast<uint16_t>(nrecv);
-  } else if (nrecv < m || m > static_cast<uint32_t>(RM)) {
+  } else if (nrecv < m || m > static_cast<uint32_t>(RM) || (a.ablate & 16u)) {
     st.state = 2;
   } else {
     // lane q < nrecv: R1 of the q-th received repair; lane c < m: S1 of missing source c
@@ -1294,7 +1309,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
       for (int w = 0; w < W; ++w) col[w] = orig[w];
       set_byte_dyn<W>(col, m - 1, ct | byte_dyn<W>(orig, m - 1));
-      if (gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
+      if ((a.ablate & 1u) || gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
     }
     if (!ok) {
       st.state = 3;
@@ -1326,8 +1341,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
           for (int s = 0; s < RM; s += 2) {
             if (static_cast<uint32_t>(s / 8) >= ntiles) break;
-            const uint32_t c0 = (v[s / 4] >> (8 * (s % 4))) & 0xFFu;
-            const uint32_t c1 = (v[(s + 1) / 4] >> (8 * ((s + 1) % 4))) & 0xFFu;
+            // ablation bit 2 (timing only): the offsets of zero coefficients, no table lookups
+            const uint32_t c0 = (a.ablate & 4u) ? 0u : (v[s / 4] >> (8 * (s % 4))) & 0xFFu;
+            const uint32_t c1 = (a.ablate & 4u) ? 0u : (v[(s + 1) / 4] >> (8 * ((s + 1) % 4))) & 0xFFu;
             jo[(s / 8) * 4 + (s % 8) / 2] = bj_quad((s % 8) / 2, c0, c1);
           }
         }
@@ -1336,14 +1352,19 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
       for (int w = 0; w < W; ++w) LO[w] = HI[w] = 0;
       auto size_terms = [&](uint32_t len, const uint32_t (&v)[W]) {
+        if (a.ablate & 8u) return;
         uint32_t tl[5], th[5];
         tab(len & 0xFFu, tl);
         tab(len >> 8, th);
 #pragma unroll
         for (int w = 0; w < W; ++w)
           if (4u * w < m) {
-            LO[w] ^= mul4(tl, v[w]);
-            HI[w] ^= mul4(th, v[w]);
+            const uint32_t s0 = v[w] & 0x07070707u, s1 = (v[w] >> 3) & 0x07070707u;
+            const uint32_t s2 = (v[w] >> 6) & 0x03030303u;
+            LO[w] ^= xor3(__builtin_amdgcn_perm(tl[1], tl[0], s0), __builtin_amdgcn_perm(tl[3], tl[2], s1),
+                          __builtin_amdgcn_perm(tl[4], tl[4], s2));
+            HI[w] ^= xor3(__builtin_amdgcn_perm(th[1], th[0], s0), __builtin_amdgcn_perm(th[3], th[2], s1),
+                          __builtin_amdgcn_perm(th[4], th[4], s2));
           }
       };
       // R1 of the repair in row q (rows 0 .. m-2: received repairs 0 .. m-2; row m-1: repair t)
@@ -1356,7 +1377,11 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         pin[q] = static_cast<uint16_t>(k + rq);
         emit(q, col);
 #pragma unroll
-        for (int w = 0; w < W; ++w) minvT[q][w] = col[w];
+        for (int w = 0; w < W; ++w) {
+          minvS[q][0][w] = col[w] & 0x07070707u;
+          minvS[q][1][w] = (col[w] >> 3) & 0x07070707u;
+          minvS[q][2][w] = (col[w] >> 6) & 0x03030303u;
+        }
         size_terms(a.rep_size[static_cast<size_t>(g) * r + rq], col);
       }
       if (lane < rp) pout[lane] = lane < m ? miss[lane] : 0;
@@ -1374,13 +1399,17 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
           uint32_t acc[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) acc[w] = 0;
-          for (uint32_t q = 0; q < m; ++q) {
+          for (uint32_t q = 0; q < ((a.ablate & 2u) ? 0u : m); ++q) {
             const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q);
             uint32_t tc[5];
             tab(((R1 + Sj) * R1) % 255u + 1u, tc);
+            const uint32_t (*sq)[W] = minvS[q];
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              if (4u * w < m) acc[w] ^= mul4(tc, minvT[q][w]);
+              if (4u * w < m)
+                acc[w] ^= xor3(__builtin_amdgcn_perm(tc[1], tc[0], sq[0][w]),
+                               __builtin_amdgcn_perm(tc[3], tc[2], sq[1][w]),
+                               __builtin_amdgcn_perm(tc[4], tc[4], sq[2][w]));
           }
           emit(pos, acc);
           size_terms(slen[j], acc);
@@ -1823,7 +1852,12 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     const char* v = std::getenv("NTC_GF256_PLAN");
     return v && !std::strcmp(v, "lds");
   }();
+  static const uint32_t ablate_w = [] {   // timing ablations of decode_plan_w (results wrong)
+    const char* v = std::getenv("NTC_GF256_PLANW_ABLATE");
+    return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
+  }();
   if (r <= 32 && !lds_plan && !ablate) {
+    p.ablate = ablate_w;
     auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;
     hipLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,
                        static_cast<hipStream_t>(stream), p);

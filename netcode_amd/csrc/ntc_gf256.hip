@@ -429,6 +429,12 @@ __global__ __launch_bounds__(256) void bj_offsets(const uint8_t* __restrict__ co
 #endif
 constexpr int kBjRing = NTC_BJ_RING;    // tuning builds: -DNTC_BJ_RING=5
 constexpr uint32_t kBjSlot = 2048;
+// NTC_BJ_LATE_READ=1: read source i from its ring slot at the top of iteration i instead of one
+// iteration ahead (8 fewer VGPRs live across the chain; tuning builds).
+#ifndef NTC_BJ_LATE_READ
+#define NTC_BJ_LATE_READ 0
+#endif
+constexpr bool kBjLateRead = NTC_BJ_LATE_READ != 0;
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p)
 {
@@ -528,20 +534,30 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jp + 16 * h);
   };
   uint32_t ycur[8];
-  vm_wait<2 * (kBjRing - 2)>();
-  ring_read(ring_p, lane, ycur);
+  if constexpr (!kBjLateRead) {
+    vm_wait<2 * (kBjRing - 2)>();
+    ring_read(ring_p, lane, ycur);
+  }
   for (uint32_t i = 0; i < k; ++i) {
     u32x16 o[NJ];
 #pragma unroll
     for (int h = 0; h < NJ; ++h) o[h] = on[h];
     uint32_t Y[kBjPlanes];
+    if constexpr (kBjLateRead) {
+      // source i's DMA has landed once only those of i+1 .. i+kBjRing-2 remain; read it straight
+      // into the planes (its LDS latency is exposed, hidden by the other waves of the SIMD)
+      vm_wait<2 * (kBjRing - 2)>();
+      ring_read(ring_p + (i % kBjRing) * kBjSlot, lane, ycur);
+    }
 #pragma unroll
     for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
     if constexpr (!(ABL & 1)) transpose8(Y);   // consume ycur before its registers are reloaded
-    // source i+1: its DMA (issued kBjRing-2 iterations ago) has landed once only the DMAs of
-    // i+2 .. i+kBjRing-2 remain; start its LDS read now, consume it next iteration
-    vm_wait<2 * (kBjRing - 3)>();
-    ring_read(ring_p + ((i + 1) % kBjRing) * kBjSlot, lane, ycur);
+    if constexpr (!kBjLateRead) {
+      // source i+1: its DMA (issued kBjRing-2 iterations ago) has landed once only the DMAs of
+      // i+2 .. i+kBjRing-2 remain; start its LDS read now, consume it next iteration
+      vm_wait<2 * (kBjRing - 3)>();
+      ring_read(ring_p + ((i + 1) % kBjRing) * kBjSlot, lane, ycur);
+    }
     {   // refill the slot of source i-1 (read and consumed) with source i + kBjRing - 1
       dma_source(nrow + x0, nrow + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
       if constexpr (DEC)
@@ -613,7 +629,11 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 constexpr int kBjWaves = NTC_BJ_WPB;     // waves (independent tasks) per workgroup; tuning builds
 
 template <int RT, bool DEC, int ABL = 0>
-__global__ __launch_bounds__(64 * kBjWaves) void gf_mac_bj(MacArgs a)
+#ifndef NTC_BJ_WAVES_PER_EU
+#define NTC_BJ_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(64 * kBjWaves)
+__attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_mac_bj(MacArgs a)
 {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[kBjWaves * kBjRing * kBjSlot];
   const uint32_t lane = threadIdx.x & 63u;

@@ -9,12 +9,12 @@ CONFS=${@:-k128r32s4096}
 B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-rate"
 envof() { [ "$1" = base ] && echo "" || echo "$1" | tr ',' ' '; }
 for v in $VARS; do
-  tag=$(echo $v | tr ',=' '__')
+  tag=$(echo $v | tr ',=/.' '____')
   timeout -k 10 300 env $(envof $v) python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/par_$tag.log 2>&1 || { tail -40 gpurun_out/par_$tag.log; exit 1; }
   echo "parity $v: $(tail -1 gpurun_out/par_$tag.log)"
 done
 for c in $CONFS; do for v in $VARS; do
-  tag=$(echo $v | tr ',=' '__')
+  tag=$(echo $v | tr ',=/.' '____')
   timeout -k 10 150 env $(envof $v) $B --config $c > gpurun_out/ab_${c}_$tag.log 2>&1
   python -c "
 import json,sys; d=json.loads(open('gpurun_out/ab_${c}_$tag.log').read().strip().splitlines()[-1])

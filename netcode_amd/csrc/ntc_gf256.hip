@@ -479,7 +479,8 @@ __device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, ui
 
 // ABL != 0: timing ablations of the encode kernel (NTC_GF256_BJ_ABLATE; results are wrong):
 // 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain,
-// 16 every source uses source 0's jump offsets (scalar-cache-resident).
+// 16 every source uses source 0's jump offsets (scalar-cache-resident), 32 every generation reads
+// generation 0's sources (L2-resident), 64 no source DMAs at all (the ring holds stale bytes).
 template <int R, int RT, bool DEC, int ABL = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
@@ -490,7 +491,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   const uint32_t c0 = cc * 2048u + lane * 16u, c1 = c0 + 1024u;
   const bool v0 = c0 < stride, v1 = c1 < stride;      // stride % 16 == 0: whole pieces
   const uint32_t x0 = v0 ? c0 : 0u, x1 = v1 ? c1 : 0u;  // invalid pieces read column 0 (unused)
-  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
+  const uint8_t* base0 = a.in0 + static_cast<size_t>((ABL & 32) ? 0u : g) * k * stride;
   const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
   const uint32_t jstep = a.ntiles * 2u * RT;
   const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * (2u * RT);
@@ -520,7 +521,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
   for (int q = 0; q < kBjRing - 1; ++q) {
     const uint8_t* row = row_at(q);
-    dma_source(row + x0, row + x1, ring + q * kBjSlot);
+    if constexpr (!(ABL & 64)) dma_source(row + x0, row + x1, ring + q * kBjSlot);
   }
   // row of source i + kBjRing - 1, the refill of iteration i (decode: loaded one iteration ahead)
   const uint8_t* nrow = row_at(kBjRing - 1);
@@ -559,7 +560,8 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
       ring_read(ring_p + ((i + 1) % kBjRing) * kBjSlot, lane, ycur);
     }
     {   // refill the slot of source i-1 (read and consumed) with source i + kBjRing - 1
-      dma_source(nrow + x0, nrow + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
+      if constexpr (!(ABL & 64))
+        dma_source(nrow + x0, nrow + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
       if constexpr (DEC)
         nrow = reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i + kBjRing));
       else
@@ -1612,6 +1614,8 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       case 8: fn = gf_mac_bj<8, false, 8>; break;
       case 11: fn = gf_mac_bj<8, false, 11>; break;
       case 16: fn = gf_mac_bj<8, false, 16>; break;
+      case 32: fn = gf_mac_bj<8, false, 32>; break;
+      case 64: fn = gf_mac_bj<8, false, 64>; break;
 
       default: break;
     }

@@ -202,9 +202,11 @@ class EncodeResult:
 class BatchEncoder:
     """G generations x (k sources -> r repairs), reference coefficient schedule."""
 
-    def __init__(self, k: int, r: int, device: int | torch.device = 0):
+    def __init__(self, k: int, r: int, device: int | torch.device = 0, engine: Engine | None = None):
+        # `engine`: a private Engine (own workspace) for launches that run concurrently with the
+        # device's shared engine on other streams (HostPipeline); default the per-device one.
         self.k, self.r = int(k), int(r)
-        self.engine = Engine.get(device)
+        self.engine = engine if engine is not None else Engine.get(device)
         self.device = self.engine.device
 
     def __call__(self, src: torch.Tensor, src_len: torch.Tensor, sid_base: torch.Tensor | None = None,
@@ -236,9 +238,11 @@ class BatchEncoder:
 class BatchDecoder:
     """In-place generation decode; returns a [G, 12] uint8 status tensor (see STATUS_DTYPE)."""
 
-    def __init__(self, k: int, r: int, device: int | torch.device = 0):
+    def __init__(self, k: int, r: int, device: int | torch.device = 0, engine: Engine | None = None):
+        # `engine`: a private Engine (own workspace) for launches that run concurrently with the
+        # device's shared engine on other streams (HostPipeline); default the per-device one.
         self.k, self.r = int(k), int(r)
-        self.engine = Engine.get(device)
+        self.engine = engine if engine is not None else Engine.get(device)
         self.device = self.engine.device
 
     def __call__(self, src: torch.Tensor, src_len: torch.Tensor, src_mask: torch.Tensor,

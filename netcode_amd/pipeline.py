@@ -1,0 +1,150 @@
+"""Host-resident batch coding: generations that start and end in pinned host memory (the
+reference's UDP socket buffers, `examples/` of ahamez/netcode) stream through the device in
+chunks, so the PCIe copies of one chunk overlap the kernels and the opposite-direction copies of
+the others.
+
+Each of `depth` slots owns a HIP stream, a private Engine (its own coefficient / plan / jump-offset
+workspace, so launches on different streams never share scratch) and device buffers for one chunk.
+Chunk c runs on slot c % depth: H2D -> encode/decode kernels -> D2H, all in stream order, so a
+slot's buffers are reused only after its previous chunk's D2H has been issued behind them.
+Results are byte-identical to one device-resident call over the whole batch (tests/
+test_gpu_pipeline.py): generations are independent and every chunk keeps its generations' id
+bases.
+"""
+from __future__ import annotations
+
+import torch
+
+from .engine import BatchDecoder, BatchEncoder, Engine, EncodeResult, STATUS_BYTES
+
+
+def _pinned(t: torch.Tensor, name: str):
+    if t.device.type != "cpu" or not t.is_pinned():
+        raise ValueError(f"{name} must be a pinned host tensor (torch.Tensor.pin_memory())")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class HostPipeline:
+    """Chunked, stream-overlapped encode / decode of host-resident generation batches."""
+
+    def __init__(self, k: int, r: int, stride: int, chunk: int, device: int | torch.device = 0,
+                 depth: int = 3):
+        if chunk <= 0 or depth <= 0:
+            raise ValueError("chunk and depth must be positive")
+        self.k, self.r, self.stride, self.chunk, self.depth = int(k), int(r), int(stride), int(chunk), int(depth)
+        dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.device = dev
+        self.streams = [torch.cuda.Stream(dev) for _ in range(depth)]
+        self.engines = [Engine(dev) for _ in range(depth)]
+        for e in self.engines:
+            e.reserve(chunk, k, r)
+        self.enc = [BatchEncoder(k, r, dev, engine=e) for e in self.engines]
+        self.dec = [BatchDecoder(k, r, dev, engine=e) for e in self.engines]
+        u8, i16 = torch.uint8, torch.int16
+        C = chunk
+        self.d_src = [torch.empty((C, k, stride), dtype=u8, device=dev) for _ in range(depth)]
+        self.d_len = [torch.empty((C, k), dtype=i16, device=dev) for _ in range(depth)]
+        self.d_mask = [torch.empty((C, k), dtype=u8, device=dev) for _ in range(depth)]
+        self.d_rmask = [torch.empty((C, r), dtype=u8, device=dev) for _ in range(depth)]
+        self.d_out = [EncodeResult(torch.empty((C, r, stride), dtype=u8, device=dev),
+                                   torch.empty((C, r), dtype=i16, device=dev),
+                                   torch.empty((C,), dtype=i16, device=dev)) for _ in range(depth)]
+        self.d_status = [torch.empty((C, STATUS_BYTES), dtype=u8, device=dev) for _ in range(depth)]
+
+    def _chunks(self, G: int):
+        for c, g0 in enumerate(range(0, G, self.chunk)):
+            yield c % self.depth, g0, min(G, g0 + self.chunk)
+
+    def _check(self, G: int, **tensors):
+        for name, t in tensors.items():
+            _pinned(t, name)
+            if t.shape[0] != G:
+                raise ValueError(f"{name}: expected {G} generations, got {t.shape[0]}")
+
+    def _ids(self, base, g0, g1):
+        return None if base is None else base[g0:g1]
+
+    def _fork(self):
+        # work the caller queued before this call (device id bases, earlier copies) comes first
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(cur)
+
+    def _join(self):
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            cur.wait_stream(s)
+
+    def encode(self, h_src, h_src_len, h_rep, h_rep_size, sid_base=None, rid_base=None):
+        """h_src [G,k,stride] u8, h_src_len [G,k] i16 -> h_rep [G,r,stride] u8, h_rep_size [G,r]
+        i16 (pinned host tensors).  sid_base / rid_base: optional device u32 [G] id bases.
+        Asynchronous with respect to the host; the caller's current stream waits for all chunks."""
+        G = h_src.shape[0]
+        self._check(G, h_src=h_src, h_src_len=h_src_len, h_rep=h_rep, h_rep_size=h_rep_size)
+        self._fork()
+        for s, g0, g1 in self._chunks(G):
+            n = g1 - g0
+            with torch.cuda.stream(self.streams[s]):
+                src, ln, out = self.d_src[s][:n], self.d_len[s][:n], self.d_out[s]
+                src.copy_(h_src[g0:g1], non_blocking=True)
+                ln.copy_(h_src_len[g0:g1], non_blocking=True)
+                o = EncodeResult(out.repairs[:n], out.encoded_size[:n], out.symbol_len[:n])
+                self.enc[s](src, ln, self._ids(sid_base, g0, g1), self._ids(rid_base, g0, g1), o)
+                h_rep[g0:g1].copy_(o.repairs, non_blocking=True)
+                h_rep_size[g0:g1].copy_(o.encoded_size, non_blocking=True)
+        self._join()
+
+    def decode(self, h_rx, h_rx_len, h_mask, h_rep, h_rep_size, h_rmask, h_status,
+               sid_base=None, rid_base=None):
+        """In-place decode of host-resident generations: received sources h_rx [G,k,stride]
+        (lost slots are overwritten with the recovered sources), h_rx_len / h_mask [G,k], repairs
+        h_rep [G,r,stride] / h_rep_size / h_rmask [G,r], status out h_status [G,12] u8."""
+        G = h_rx.shape[0]
+        self._check(G, h_rx=h_rx, h_rx_len=h_rx_len, h_mask=h_mask, h_rep=h_rep,
+                    h_rep_size=h_rep_size, h_rmask=h_rmask, h_status=h_status)
+        self._fork()
+        for s, g0, g1 in self._chunks(G):
+            n = g1 - g0
+            with torch.cuda.stream(self.streams[s]):
+                rx, ln, mk = self.d_src[s][:n], self.d_len[s][:n], self.d_mask[s][:n]
+                rep, rsz, rmk = self.d_out[s].repairs[:n], self.d_out[s].encoded_size[:n], self.d_rmask[s][:n]
+                st = self.d_status[s][:n]
+                for d, h in ((rx, h_rx), (ln, h_rx_len), (mk, h_mask), (rep, h_rep), (rsz, h_rep_size),
+                             (rmk, h_rmask)):
+                    d.copy_(h[g0:g1], non_blocking=True)
+                self.dec[s](rx, ln, mk, rep, rsz, rmk, self._ids(sid_base, g0, g1),
+                            self._ids(rid_base, g0, g1), st)
+                h_rx[g0:g1].copy_(rx, non_blocking=True)
+                h_status[g0:g1].copy_(st, non_blocking=True)
+        self._join()
+
+    def encode_decode(self, h_src, h_src_len, h_rep, h_rep_size, h_rx, h_rx_len, h_mask, h_rmask,
+                      h_status, sid_base=None, rid_base=None):
+        """Loopback of one batch (bench.py's host-resident rate): per chunk, sources H2D -> encode
+        -> repairs D2H to h_rep, then received sources H2D -> decode with the chunk's repairs
+        still on the device -> recovered sources and status D2H.  Same results as encode() then
+        decode() with h_rep as the decoder's repairs."""
+        G = h_src.shape[0]
+        self._check(G, h_src=h_src, h_src_len=h_src_len, h_rep=h_rep, h_rep_size=h_rep_size,
+                    h_rx=h_rx, h_rx_len=h_rx_len, h_mask=h_mask, h_rmask=h_rmask, h_status=h_status)
+        self._fork()
+        for s, g0, g1 in self._chunks(G):
+            n = g1 - g0
+            with torch.cuda.stream(self.streams[s]):
+                buf, ln, mk, rmk = self.d_src[s][:n], self.d_len[s][:n], self.d_mask[s][:n], self.d_rmask[s][:n]
+                out, st = self.d_out[s], self.d_status[s][:n]
+                o = EncodeResult(out.repairs[:n], out.encoded_size[:n], out.symbol_len[:n])
+                sid, rid = self._ids(sid_base, g0, g1), self._ids(rid_base, g0, g1)
+                buf.copy_(h_src[g0:g1], non_blocking=True)
+                ln.copy_(h_src_len[g0:g1], non_blocking=True)
+                self.enc[s](buf, ln, sid, rid, o)
+                h_rep[g0:g1].copy_(o.repairs, non_blocking=True)
+                h_rep_size[g0:g1].copy_(o.encoded_size, non_blocking=True)
+                # the decoder's slots reuse the source buffer (stream order: the encode has read it)
+                for d, h in ((buf, h_rx), (ln, h_rx_len), (mk, h_mask), (rmk, h_rmask)):
+                    d.copy_(h[g0:g1], non_blocking=True)
+                self.dec[s](buf, ln, mk, o.repairs, o.encoded_size, rmk, sid, rid, st)
+                h_rx[g0:g1].copy_(buf, non_blocking=True)
+                h_status[g0:g1].copy_(st, non_blocking=True)
+        self._join()

@@ -136,8 +136,11 @@ def tables(y, R, safe):
 
 def chain_lines(y, R):
     span = 2 * R * SITE
+    # NTC_BJ_EXTRA_SALU=n (timing experiment only): n dummy scalar ops per chain entry
+    extra = ["s_add_u32 s96, s96, 0"] * int(os.environ.get("NTC_BJ_EXTRA_SALU", "0"))
     lines = ["s_getpc_b64 s[96:97]", "Lg%=:",
-             "s_add_u32 s96, s96, Ltf%= - Lg%=", "s_addc_u32 s97, s97, 0",
+             "s_add_u32 s96, s96, Ltf%= - Lg%=", "s_addc_u32 s97, s97, 0"] + extra + [
+
              # fast path iff [Ltf, Ltf + span) does not cross a 4 GiB boundary
              f"s_add_u32 s98, s96, {span}", "s_cbranch_scc1 Lsafe%=",
              "s_mov_b32 s99, s97",

@@ -43,7 +43,7 @@ typedef enum {
   NTC_GPU_EINVAL = 1,        /* bad argument (sizes, alignment, NULL) */
   NTC_GPU_ENOMEM = 2,        /* device workspace allocation failed */
   NTC_GPU_EDEVICE = 3,       /* HIP runtime error (launch / device) */
-  NTC_GPU_EUNSUPPORTED = 4   /* shape outside this build's limits (e.g. r > 64) */
+  NTC_GPU_EUNSUPPORTED = 4   /* shape outside this build's limits (e.g. decode r > 255) */
 } ntc_gpu_status;
 
 /* Per-generation decode outcome; the same fields the reference decoder's counters expose
@@ -92,7 +92,8 @@ int  ntc_gf256_encode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint3
 
 /* Decode in place: lost source slots (src_mask == 0) whose generation decodes are overwritten
  * with the recovered payload (zero-padded to stride) and their src_len set to the decoded size.
- * status[g] receives the outcome.  Requires r <= 64 (m <= 64). */
+ * status[g] receives the outcome.  Requires r <= 255 (r <= 64: wave-level plan kernels; 64 < r
+ * <= 255: one workgroup per generation, decode_plan_big). */
 int  ntc_gf256_decode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,
                             uint32_t stride, uint8_t* src, uint16_t* src_len,
                             const uint8_t* src_mask, const uint8_t* rep, const uint16_t* rep_size,

@@ -35,7 +35,7 @@ __constant__ __attribute__((aligned(16))) PermTables d_perm = make_perm_tables()
 __constant__ __attribute__((aligned(16))) FieldTables d_field = make_field_tables();
 
 constexpr int kWaves = 4;               // waves per 256-thread block
-constexpr int kMaxPlanRows = 64;        // m <= 64 (r <= 64) in this build
+constexpr int kMaxPlanRows = 64;        // r <= 64: wave-level plan kernels; larger r: decode_plan_big
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -1142,6 +1142,198 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   }
 }
 
+// ------------------------------------------------------------ decode plan, 64 < r <= 255 ----
+// Large windows (m up to 255, the w = 8 limit): one 256-thread workgroup per
+// generation, the augmented matrix [M | I] (m x 2m bytes) in LDS with thread = row.  Same
+// greedy retry (decoder.cc:448-468), status, decoded sizes (:484-497) and plan layout as
+// decode_plan; the jump offsets of the bit-sliced MAC come from bj_offsets at apply time.
+// Windows this large are rare, so this kernel favours simplicity over speed (block barriers per
+// pivot), but every step stays on the device.
+constexpr uint32_t kBigRows = 255;
+constexpr uint32_t kBigPitch = 129;          // dwords per row: 2 * 256 bytes / 4, +1 (banks)
+
+__global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t big_lds[];
+  uint32_t (*A)[kBigPitch] = reinterpret_cast<uint32_t (*)[kBigPitch]>(big_lds);
+  uint16_t* miss = reinterpret_cast<uint16_t*>(big_lds + 256 * kBigPitch);   // [256]
+  uint16_t* recv = miss + 256;                                             // [256]
+  uint16_t* reps = recv + 256;                                             // [256]
+  uint16_t* rl = reps + 256;                                               // [256] chunk list
+  uint32_t* szs = reinterpret_cast<uint32_t*>(rl + 256);                   // [256]
+  uint32_t* wcnt = szs + 256;                                              // [4] + [1]
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t g = blockIdx.x;
+  const uint32_t k = a.k, r = a.r;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
+  const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
+  const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+
+  // Ordered block-wide compaction of the indices in [base, base + 256) satisfying `pred`, appended
+  // to out[] from position `n` (entries past `cap` are dropped); returns how many satisfied it.
+  auto compact = [&](uint32_t base, uint32_t end, bool lost, const uint8_t* msk, uint16_t* out,
+                     uint32_t n, uint32_t cap) -> uint32_t {
+    const uint32_t idx = base + tid;
+    const bool hit = idx < end && ((msk[idx] == 0) == lost);
+    const uint64_t b = __ballot(hit);
+    if (lane == 0) wcnt[wv] = __popcll(b);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+      if (w < wv) off += wcnt[w];
+      tot += wcnt[w];
+    }
+    if (hit) {
+      const uint32_t pos = n + off + __popcll(b & lt);
+      if (pos < cap) out[pos] = static_cast<uint16_t>(idx);
+    }
+    __syncthreads();
+    return tot;
+  };
+
+  uint32_t m = 0;
+  for (uint32_t base = 0; base < k; base += 256) m += compact(base, k, true, smask, miss, m, 256);
+  const uint32_t nrecv = compact(0, r, false, rmask, recv, 0, 256);
+
+  ntc_gf256_decode_status st{};
+  st.nb_missing = static_cast<uint16_t>(m);
+  st.last_repair = 0xFFFF;
+  uint32_t mm = 0;
+  if (m == 0) {
+    st.state = 1;
+    st.nb_useless = static_cast<uint16_t>(nrecv);
+  } else if (nrecv < m || m > kBigRows) {
+    st.state = 2;
+  } else {
+    const uint32_t nw = (2 * m + 3) / 4;
+    auto byte_at = [&](uint32_t row, uint32_t c) -> uint32_t {
+      return (A[row][c >> 2] >> (8 * (c & 3))) & 0xFFu;
+    };
+    bool ok = false;
+    uint32_t t = m - 1;
+    for (; t < nrecv; ++t) {
+      if (tid < m) {       // thread q builds row q: coefficients of the missing sources | identity
+        const uint32_t rq = (tid + 1 < m) ? recv[tid] : recv[t];
+        reps[tid] = static_cast<uint16_t>(rq);
+        const uint32_t rid = ridb + rq;
+        for (uint32_t w = 0; w < nw; ++w) {
+          uint32_t word = 0;
+          for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t c = 4 * w + b;
+            uint32_t v = 0;
+            if (c < m) v = coefficient(rid, sidb + miss[c]);
+            else if (c < 2 * m) v = (c - m == tid) ? 1u : 0u;
+            word |= v << (8 * b);
+          }
+          A[tid][w] = word;
+        }
+      }
+      __syncthreads();
+      bool singular = false;
+      for (uint32_t p = 0; p < m; ++p) {
+        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid >= p && tid < m && byte_at(tid, p) != 0) atomicMin(&wcnt[4], tid);
+        __syncthreads();
+        const uint32_t q = wcnt[4];
+        if (q == 0xFFFFFFFFu) { singular = true; break; }
+        if (q != p) {
+          for (uint32_t w = tid; w < nw; w += 256) {
+            const uint32_t tmp = A[p][w];
+            A[p][w] = A[q][w];
+            A[q][w] = tmp;
+          }
+          __syncthreads();
+        }
+        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(p, p))];
+        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
+        for (uint32_t w = tid; w < nw; w += 256) A[p][w] = mul4(tinv, A[p][w]);
+        __syncthreads();
+        const uint32_t fa = (tid < m && tid != p) ? byte_at(tid, p) : 0u;
+        if (fa != 0) {
+          const uint32_t* tf0 = d_perm.w[fa];
+          const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
+          for (uint32_t w = 0; w < nw; ++w) A[tid][w] ^= mul4(tf, A[p][w]);
+        }
+        __syncthreads();
+      }
+      if (!singular) { ok = true; break; }
+      __syncthreads();
+    }
+    if (!ok) {
+      st.state = 3;
+      const uint32_t f = nrecv - m + 1;
+      st.nb_failed = static_cast<uint8_t>(f > 255 ? 255 : f);
+    } else {
+      st.state = 0;
+      const uint32_t f = t - (m - 1);
+      st.nb_failed = static_cast<uint8_t>(f > 255 ? 255 : f);
+      st.nb_decoded = static_cast<uint16_t>(m);
+      st.nb_useless = static_cast<uint16_t>(nrecv - 1 - t);
+      st.last_repair = recv[t];
+      mm = m;
+      const uint32_t rp = a.rp;
+      uint16_t* pin = a.plan_in + static_cast<size_t>(g) * k;
+      uint8_t* pc = a.plan_coef + static_cast<size_t>(g) * k * rp;
+      uint16_t* pout = a.plan_out + static_cast<size_t>(g) * rp;
+      uint16_t* slen = a.src_len + static_cast<size_t>(g) * k;
+      auto minv = [&](uint32_t s, uint32_t q) -> uint32_t { return byte_at(s, m + q); };
+      for (uint32_t s = tid; s < rp; s += 256) pout[s] = (s < m) ? miss[s] : 0;
+      // positions 0 .. m-1: the chosen repairs, D[s][q] = (M^-1)[s][q]; thread = output row s
+      for (uint32_t q = 0; q < m; ++q) {
+        if (tid == 0) pin[q] = static_cast<uint16_t>(k + reps[q]);
+        for (uint32_t s = tid; s < rp; s += 256)
+          pc[static_cast<size_t>(q) * rp + s] = static_cast<uint8_t>(s < m ? minv(s, q) : 0u);
+      }
+      // reduced encoded sizes (decoder.cc:402-404): thread q owns repair q
+      uint32_t red = 0;
+      if (tid < m) {
+        const uint32_t rid = ridb + reps[tid];
+        red = a.rep_size[static_cast<size_t>(g) * r + reps[tid]];
+        for (uint32_t j = 0; j < k; ++j)
+          if (smask[j]) red ^= mul_size(slen[j], static_cast<uint8_t>(coefficient(rid, sidb + j)));
+        szs[tid] = red;
+      }
+      __syncthreads();
+      // positions m .. k-1: received sources ascending, D[s][j] = sum_q (M^-1)[s][q] c(q, j)
+      uint32_t pos = m;
+      for (uint32_t base = 0; base < k; base += 256) {
+        const uint32_t cnt = compact(base, k, false, smask, rl, 0, 256);
+        for (uint32_t i = tid; i < cnt; i += 256) pin[pos + i] = rl[i];
+        for (uint32_t i = 0; i < cnt; ++i) {
+          const uint32_t j = rl[i];
+          for (uint32_t s = tid; s < rp; s += 256) {
+            uint32_t d = 0;
+            if (s < m)
+              for (uint32_t q = 0; q < m; ++q)
+                d ^= gmul(static_cast<uint8_t>(minv(s, q)),
+                          static_cast<uint8_t>(coefficient(ridb + reps[q], sidb + j)));
+            pc[static_cast<size_t>(pos + i) * rp + s] = static_cast<uint8_t>(d);
+          }
+        }
+        pos += cnt;
+        __syncthreads();
+      }
+      // decoded size of missing source s = sum_q (M^-1)[s][q] (x) reduced size of repair q
+      if (tid < m) {
+        uint32_t sz = 0;
+        for (uint32_t q = 0; q < m; ++q) sz ^= mul_size(static_cast<uint16_t>(szs[q]),
+                                                       static_cast<uint8_t>(minv(tid, q)));
+        slen[miss[tid]] = static_cast<uint16_t>(sz);
+      }
+    }
+  }
+  if (tid == 0) {
+    a.plan_m[g] = static_cast<uint16_t>(mm);
+    a.status[g] = st;
+  }
+}
+// dynamic LDS of decode_plan_big: matrix + miss/recv/reps/rl (u16) + szs + 5 counters (u32)
+constexpr size_t kBigLds = (256 * kBigPitch + 4 * 128 + 256 + 8) * 4;
+
 // ------------------------------------------------------------- decode plan, r <= 32 (v2) ----
 // Register-resident decode_plan for r <= 32 (config 3 and every shape with at most 32 repairs):
 // one wave per generation, four generations per block sharing one LDS copy of the v_perm tables.
@@ -1847,7 +2039,9 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
   if (!e || !src_len || !src_mask || !rep_size || !rep_mask || !status)
     return fail(NTC_GPU_EINVAL, "NULL argument");
   if (G == 0 || k == 0) return fail(NTC_GPU_EINVAL, "G and k must be > 0");
-  if (r > static_cast<uint32_t>(kMaxPlanRows)) return fail(NTC_GPU_EUNSUPPORTED, "r > 64 not supported by decode");
+  if (r > kBigRows) return fail(NTC_GPU_EUNSUPPORTED, "r > 255 not supported by decode (w = 8 limit)");
+  const bool big = r > static_cast<uint32_t>(kMaxPlanRows);    // decode_plan_big
+  if (big) offsets = false;                 // apply computes the bit-sliced offsets (bj_offsets)
   if (k > 65535) return fail(NTC_GPU_EUNSUPPORTED, "k > 65535");
   const uint32_t rp = tile_rp(r);
   (void)hipSetDevice(e->device);
@@ -1880,7 +2074,16 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     const char* v = std::getenv("NTC_GF256_PLANW_ABLATE");
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
-  if (r <= 32 && !lds_plan && !ablate) {
+  if (big) {
+    static const int lds_ok = [] {
+      return static_cast<int>(hipFuncSetAttribute(reinterpret_cast<const void*>(decode_plan_big),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  static_cast<int>(kBigLds)));
+    }();
+    if (lds_ok != 0) return fail(NTC_GPU_EDEVICE, "decode_plan_big: LDS attribute");
+    hipLaunchKernelGGL(decode_plan_big, dim3(G), dim3(256), kBigLds,
+                       static_cast<hipStream_t>(stream), p);
+  } else if (r <= 32 && !lds_plan && !ablate) {
     p.ablate = ablate_w;
     auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;
     hipLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,

@@ -836,6 +836,7 @@ struct PlanArgs {
   uint32_t ablate;   // tuning only: bit0 skip elimination, bit1 skip D for received sources
   uint32_t* joff;    // non-null: also write the bit-sliced MAC's jump offsets (8-row tiles)
   uint32_t ntiles;
+  uint32_t big_rows, big_pitch;   // decode_plan_big: LDS matrix shape
 };
 
 // Jump offsets of one (input position, 8-row tile, 2-row quad) from the two rows' coefficients
@@ -1150,18 +1151,27 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
 // Windows this large are rare, so this kernel favours simplicity over speed (block barriers per
 // pivot), but every step stays on the device.
 constexpr uint32_t kBigRows = 255;
-constexpr uint32_t kBigPitch = 129;          // dwords per row: 2 * 256 bytes / 4, +1 (banks)
 
 __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t big_lds[];
-  uint32_t (*A)[kBigPitch] = reinterpret_cast<uint32_t (*)[kBigPitch]>(big_lds);
-  uint16_t* miss = reinterpret_cast<uint16_t*>(big_lds + 256 * kBigPitch);   // [256]
+  // A: a.big_rows rows (>= r) of a.big_pitch dwords (>= 2r bytes, odd: conflict-free per row),
+  // sized per launch so small windows fit several workgroups per CU
+  const uint32_t P = a.big_pitch;
+  uint32_t* A = big_lds;
+  uint16_t* miss = reinterpret_cast<uint16_t*>(big_lds + a.big_rows * P);  // [256]
   uint16_t* recv = miss + 256;                                             // [256]
   uint16_t* reps = recv + 256;                                             // [256]
   uint16_t* rl = reps + 256;                                               // [256] chunk list
-  uint32_t* szs = reinterpret_cast<uint32_t*>(rl + 256);                   // [256]
-  uint32_t* wcnt = szs + 256;                                              // [4] + [1]
+  uint16_t* sl = rl + 256;                                                 // [256] its lengths
+  uint32_t* szs = reinterpret_cast<uint32_t*>(sl + 256);                   // [256]
+  uint32_t* wcnt = szs + 256;                                              // [4] + [1] (+3)
+  uint32_t (*ptab)[8] = reinterpret_cast<uint32_t (*)[8]>(wcnt + 8);       // v_perm tables, 8 KiB
+  {   // per-thread coefficients index the tables divergently: serve them from LDS
+    const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
+    for (uint32_t i = threadIdx.x; i < 512u; i += 256u) dst[i] = src[i];
+  }
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t g = blockIdx.x;
@@ -1210,11 +1220,73 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
   } else {
     const uint32_t nw = (2 * m + 3) / 4;
     auto byte_at = [&](uint32_t row, uint32_t c) -> uint32_t {
-      return (A[row][c >> 2] >> (8 * (c & 3))) & 0xFFu;
+      return (A[(row) * P + (c >> 2)] >> (8 * (c & 3))) & 0xFFu;
     };
     bool ok = false;
     uint32_t t = m - 1;
-    for (; t < nrecv; ++t) {
+    // Screening (same outcome as trying t = m-1, m, ... with a full Gauss-Jordan each, as
+    // decoder.cc:448-468 does): {first m-1 repairs} + {t} is invertible iff the first m-1 rows
+    // are independent and row t is outside their span.  One forward elimination over all
+    // received rows (pivots chosen among the first m-1 only) leaves every candidate row reduced
+    // against that basis; the first nonzero one is the repair that completes decoding.
+    bool found = false;
+    {
+      const uint32_t nwl = (m + 3) / 4;
+      if (tid < nrecv) {   // row i: received repair i over the missing sources
+        const uint32_t rid = ridb + recv[tid];
+        for (uint32_t w = 0; w < nwl; ++w) {
+          uint32_t word = 0;
+          for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t c = 4 * w + b;
+            if (c < m) word |= coefficient(rid, sidb + miss[c]) << (8 * b);
+          }
+          A[(tid) * P + (w)] = word;
+        }
+      }
+      __syncthreads();
+      uint32_t rank = 0;
+      for (uint32_t c = 0; c < m && rank + 1 < m; ++c) {
+        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid >= rank && tid + 1 < m && byte_at(tid, c) != 0) atomicMin(&wcnt[4], tid);
+        __syncthreads();
+        const uint32_t q = wcnt[4];
+        if (q == 0xFFFFFFFFu) continue;               // no pivot in this column (uniform)
+        if (q != rank) {
+          for (uint32_t w = tid; w < nwl; w += 256) {
+            const uint32_t tmp = A[(rank) * P + (w)];
+            A[(rank) * P + (w)] = A[(q) * P + (w)];
+            A[(q) * P + (w)] = tmp;
+          }
+          __syncthreads();
+        }
+        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(rank, c))];
+        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
+        for (uint32_t w = tid; w < nwl; w += 256) A[(rank) * P + (w)] = mul4(tinv, A[(rank) * P + (w)]);
+        __syncthreads();
+        const uint32_t fa = (tid > rank && tid < nrecv) ? byte_at(tid, c) : 0u;
+        if (fa != 0)
+          for (uint32_t w = 0; w < nwl; ++w) A[(tid) * P + (w)] ^= mul4(ptab[fa], A[(rank) * P + (w)]);
+        __syncthreads();
+        ++rank;
+      }
+      if (rank + 1 == m) {
+        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid + 1 >= m && tid < nrecv) {
+          uint32_t nz = 0;
+          for (uint32_t w = 0; w < nwl; ++w) nz |= A[(tid) * P + (w)];
+          if (nz != 0) atomicMin(&wcnt[4], tid);
+        }
+        __syncthreads();
+        if (wcnt[4] != 0xFFFFFFFFu) {
+          found = true;
+          t = wcnt[4];
+        }
+      }
+      __syncthreads();
+    }
+    for (; found && t < nrecv; ++t) {   // one iteration: M^-1 for the chosen candidate
       if (tid < m) {       // thread q builds row q: coefficients of the missing sources | identity
         const uint32_t rq = (tid + 1 < m) ? recv[tid] : recv[t];
         reps[tid] = static_cast<uint16_t>(rq);
@@ -1228,7 +1300,7 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
             else if (c < 2 * m) v = (c - m == tid) ? 1u : 0u;
             word |= v << (8 * b);
           }
-          A[tid][w] = word;
+          A[(tid) * P + (w)] = word;
         }
       }
       __syncthreads();
@@ -1242,26 +1314,26 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         if (q == 0xFFFFFFFFu) { singular = true; break; }
         if (q != p) {
           for (uint32_t w = tid; w < nw; w += 256) {
-            const uint32_t tmp = A[p][w];
-            A[p][w] = A[q][w];
-            A[q][w] = tmp;
+            const uint32_t tmp = A[(p) * P + (w)];
+            A[(p) * P + (w)] = A[(q) * P + (w)];
+            A[(q) * P + (w)] = tmp;
           }
           __syncthreads();
         }
         const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(p, p))];
         const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
-        for (uint32_t w = tid; w < nw; w += 256) A[p][w] = mul4(tinv, A[p][w]);
+        for (uint32_t w = tid; w < nw; w += 256) A[(p) * P + (w)] = mul4(tinv, A[(p) * P + (w)]);
         __syncthreads();
         const uint32_t fa = (tid < m && tid != p) ? byte_at(tid, p) : 0u;
         if (fa != 0) {
-          const uint32_t* tf0 = d_perm.w[fa];
+          const uint32_t* tf0 = ptab[fa];
           const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
-          for (uint32_t w = 0; w < nw; ++w) A[tid][w] ^= mul4(tf, A[p][w]);
+          for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(p) * P + (w)]);
         }
         __syncthreads();
       }
-      if (!singular) { ok = true; break; }
-      __syncthreads();
+      ok = !singular;
+      break;
     }
     if (!ok) {
       st.state = 3;
@@ -1288,40 +1360,40 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         for (uint32_t s = tid; s < rp; s += 256)
           pc[static_cast<size_t>(q) * rp + s] = static_cast<uint8_t>(s < m ? minv(s, q) : 0u);
       }
-      // reduced encoded sizes (decoder.cc:402-404): thread q owns repair q
-      uint32_t red = 0;
-      if (tid < m) {
-        const uint32_t rid = ridb + reps[tid];
-        red = a.rep_size[static_cast<size_t>(g) * r + reps[tid]];
-        for (uint32_t j = 0; j < k; ++j)
-          if (smask[j]) red ^= mul_size(slen[j], static_cast<uint8_t>(coefficient(rid, sidb + j)));
-        szs[tid] = red;
-      }
-      __syncthreads();
+      // reduced encoded sizes (decoder.cc:402-404), accumulated per chunk below: thread q owns
+      // repair q; one mul4 codes both bytes of a u16 length (galois_field.hh:108-115)
+      uint32_t red = tid < m ? a.rep_size[static_cast<size_t>(g) * r + reps[tid]] : 0u;
+      const uint32_t rid_t = tid < m ? ridb + reps[tid] : 0u;
       // positions m .. k-1: received sources ascending, D[s][j] = sum_q (M^-1)[s][q] c(q, j)
       uint32_t pos = m;
       for (uint32_t base = 0; base < k; base += 256) {
         const uint32_t cnt = compact(base, k, false, smask, rl, 0, 256);
-        for (uint32_t i = tid; i < cnt; i += 256) pin[pos + i] = rl[i];
+        for (uint32_t i = tid; i < cnt; i += 256) {
+          pin[pos + i] = rl[i];
+          sl[i] = slen[rl[i]];
+        }
+        __syncthreads();
+        if (tid < m)
+          for (uint32_t i = 0; i < cnt; ++i) red ^= mul4(ptab[coefficient(rid_t, sidb + rl[i])], sl[i]);
         for (uint32_t i = 0; i < cnt; ++i) {
           const uint32_t j = rl[i];
           for (uint32_t s = tid; s < rp; s += 256) {
             uint32_t d = 0;
             if (s < m)
               for (uint32_t q = 0; q < m; ++q)
-                d ^= gmul(static_cast<uint8_t>(minv(s, q)),
-                          static_cast<uint8_t>(coefficient(ridb + reps[q], sidb + j)));
+                d ^= mul4(ptab[coefficient(ridb + reps[q], sidb + j)], minv(s, q));
             pc[static_cast<size_t>(pos + i) * rp + s] = static_cast<uint8_t>(d);
           }
         }
         pos += cnt;
         __syncthreads();
       }
+      if (tid < m) szs[tid] = red & 0xFFFFu;
+      __syncthreads();
       // decoded size of missing source s = sum_q (M^-1)[s][q] (x) reduced size of repair q
       if (tid < m) {
         uint32_t sz = 0;
-        for (uint32_t q = 0; q < m; ++q) sz ^= mul_size(static_cast<uint16_t>(szs[q]),
-                                                       static_cast<uint8_t>(minv(tid, q)));
+        for (uint32_t q = 0; q < m; ++q) sz ^= mul4(ptab[minv(tid, q)], szs[q]);
         slen[miss[tid]] = static_cast<uint16_t>(sz);
       }
     }
@@ -1331,8 +1403,12 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
     a.status[g] = st;
   }
 }
-// dynamic LDS of decode_plan_big: matrix + miss/recv/reps/rl (u16) + szs + 5 counters (u32)
-constexpr size_t kBigLds = (256 * kBigPitch + 4 * 128 + 256 + 8) * 4;
+// dynamic LDS of decode_plan_big: matrix + miss/recv/reps/rl (u16) + szs + counters + v_perm tables
+// (big_rows * big_pitch is padded to a multiple of 4 dwords, so ptab stays 16-byte aligned)
+inline size_t big_lds_bytes(uint32_t rows, uint32_t pitch)
+{
+  return (static_cast<size_t>(rows) * pitch + 5 * 128 + 256 + 8 + 256 * 8) * 4;
+}
 
 // ------------------------------------------------------------- decode plan, r <= 32 (v2) ----
 // Register-resident decode_plan for r <= 32 (config 3 and every shape with at most 32 repairs):
@@ -2075,13 +2151,16 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
   if (big) {
+    p.big_pitch = ((2 * r + 3) / 4) | 1u;
+    p.big_rows = r;
+    while ((p.big_rows * p.big_pitch) % 4u) ++p.big_rows;
     static const int lds_ok = [] {
       return static_cast<int>(hipFuncSetAttribute(reinterpret_cast<const void*>(decode_plan_big),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  static_cast<int>(kBigLds)));
+                                                  static_cast<int>(big_lds_bytes(260, 129))));
     }();
     if (lds_ok != 0) return fail(NTC_GPU_EDEVICE, "decode_plan_big: LDS attribute");
-    hipLaunchKernelGGL(decode_plan_big, dim3(G), dim3(256), kBigLds,
+    hipLaunchKernelGGL(decode_plan_big, dim3(G), dim3(256), big_lds_bytes(p.big_rows, p.big_pitch),
                        static_cast<hipStream_t>(stream), p);
   } else if (r <= 32 && !lds_plan && !ablate) {
     p.ablate = ablate_w;

@@ -1167,6 +1167,7 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
   uint32_t* szs = reinterpret_cast<uint32_t*>(sl + 256);                   // [256]
   uint32_t* wcnt = szs + 256;                                              // [4] + [1] (+3)
   uint32_t (*ptab)[8] = reinterpret_cast<uint32_t (*)[8]>(wcnt + 8);       // v_perm tables, 8 KiB
+  uint32_t* c4 = &ptab[0][0] + 256 * 8;       // [m][8]: c(q, j) of 32 received positions, packed
   {   // per-thread coefficients index the tables divergently: serve them from LDS
     const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
@@ -1375,14 +1376,42 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         __syncthreads();
         if (tid < m)
           for (uint32_t i = 0; i < cnt; ++i) red ^= mul4(ptab[coefficient(rid_t, sidb + rl[i])], sl[i]);
-        for (uint32_t i = 0; i < cnt; ++i) {
-          const uint32_t j = rl[i];
+        // 32 positions at a time: thread s takes the table of (M^-1)[s][q] once per q and
+        // multiplies four positions' coefficients c(q, j..j+3) per mul4
+        for (uint32_t i0 = 0; i0 < cnt; i0 += 32) {
+          const uint32_t n32 = min(32u, cnt - i0);
+          __syncthreads();                      // the previous block's c4 reads are done
+          for (uint32_t e = tid; e < m * 8u; e += 256) {
+            const uint32_t q = e >> 3, w = e & 7u;
+            const uint32_t rid = ridb + reps[q];
+            uint32_t word = 0;
+            for (uint32_t b = 0; b < 4; ++b) {
+              const uint32_t i = i0 + 4 * w + b;
+              if (i < cnt) word |= coefficient(rid, sidb + rl[i]) << (8 * b);
+            }
+            c4[e] = word;
+          }
+          __syncthreads();
           for (uint32_t s = tid; s < rp; s += 256) {
-            uint32_t d = 0;
+            uint32_t acc[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) acc[w] = 0;
             if (s < m)
-              for (uint32_t q = 0; q < m; ++q)
-                d ^= mul4(ptab[coefficient(ridb + reps[q], sidb + j)], minv(s, q));
-            pc[static_cast<size_t>(pos + i) * rp + s] = static_cast<uint8_t>(d);
+              for (uint32_t q = 0; q < m; ++q) {
+                const uint32_t* tq = ptab[minv(s, q)];
+                const uint32_t tt[5] = {tq[0], tq[1], tq[2], tq[3], tq[4]};
+                const uint4 lo = *reinterpret_cast<const uint4*>(c4 + q * 8);
+                const uint4 hi = *reinterpret_cast<const uint4*>(c4 + q * 8 + 4);
+                acc[0] ^= mul4(tt, lo.x); acc[1] ^= mul4(tt, lo.y);
+                acc[2] ^= mul4(tt, lo.z); acc[3] ^= mul4(tt, lo.w);
+                acc[4] ^= mul4(tt, hi.x); acc[5] ^= mul4(tt, hi.y);
+                acc[6] ^= mul4(tt, hi.z); acc[7] ^= mul4(tt, hi.w);
+              }
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+              if (static_cast<uint32_t>(i) < n32)
+                pc[static_cast<size_t>(pos + i0 + i) * rp + s] =
+                    static_cast<uint8_t>(acc[i >> 2] >> (8 * (i & 3)));
           }
         }
         pos += cnt;
@@ -1407,7 +1436,7 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
 // (big_rows * big_pitch is padded to a multiple of 4 dwords, so ptab stays 16-byte aligned)
 inline size_t big_lds_bytes(uint32_t rows, uint32_t pitch)
 {
-  return (static_cast<size_t>(rows) * pitch + 5 * 128 + 256 + 8 + 256 * 8) * 4;
+  return (static_cast<size_t>(rows) * pitch + 5 * 128 + 256 + 8 + 256 * 8 + 256 * 8) * 4;
 }
 
 // ------------------------------------------------------------- decode plan, r <= 32 (v2) ----

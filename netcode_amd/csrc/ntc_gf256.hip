@@ -2145,7 +2145,12 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     return fail(NTC_GPU_EINVAL, "NULL argument");
   if (G == 0 || k == 0) return fail(NTC_GPU_EINVAL, "G and k must be > 0");
   if (r > kBigRows) return fail(NTC_GPU_EUNSUPPORTED, "r > 255 not supported by decode (w = 8 limit)");
-  const bool big = r > static_cast<uint32_t>(kMaxPlanRows);    // decode_plan_big
+  // NTC_GF256_PLAN=big: decode_plan_big for every r (A/B and coverage of the big kernel)
+  static const bool force_big = [] {
+    const char* v = std::getenv("NTC_GF256_PLAN");
+    return v && !std::strcmp(v, "big");
+  }();
+  const bool big = r > static_cast<uint32_t>(kMaxPlanRows) || (force_big && r > 0);
   if (big) offsets = false;                 // apply computes the bit-sliced offsets (bj_offsets)
   if (k > 65535) return fail(NTC_GPU_EUNSUPPORTED, "k > 65535");
   const uint32_t rp = tile_rp(r);

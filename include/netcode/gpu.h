@@ -73,11 +73,32 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
 enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2 };
 int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);
 
+/* Decode-plan kernel (coverage and A/B testing; results are identical).  AUTO: the register-
+ * resident wave plan for r <= 32, the LDS wave plan for r <= 64, the workgroup plan above; WAVE /
+ * LDS fall back to the next kernel when r exceeds their limit (32 / 64); BIG forces the
+ * workgroup plan for every r.  The NTC_GF256_PLAN=lds|big environment variable overrides AUTO. */
+enum { NTC_GF256_PLAN_AUTO = 0, NTC_GF256_PLAN_WAVE = 1, NTC_GF256_PLAN_LDS = 2,
+       NTC_GF256_PLAN_BIG = 3 };
+int  ntc_gf256_set_plan_kind(ntc_gf256_engine* eng, int kind);
+
 /* Profiling: with timing on, the engine records HIP events on the caller's stream around each
  * region-MAC kernel launch; ntc_gf256_mac_time waits for the last encode (dec = 0) or decode
  * (dec = 1) MAC and returns that kernel's duration in ms. */
 int  ntc_gf256_set_timing(ntc_gf256_engine* eng, int on);
 int  ntc_gf256_mac_time(ntc_gf256_engine* eng, int dec, float* ms);
+
+/* Kernel timing log: after ntc_gf256_timing_log(eng, capacity > 0) the engine brackets each of
+ * the next `capacity` kernels it launches with a HIP event pair on the launch stream (capacity 0
+ * turns the log off; every call clears it).  ntc_gf256_timing_read waits for the logged kernels
+ * and returns up to `max` entries in launch order: kinds[i] (NTC_GF256_K_*) and ms[i] (that
+ * kernel's duration); *n = entries logged.  bench.py times the kernels of its timed steps this
+ * way, so per-step kernel sums come from the same launches as the step time. */
+enum { NTC_GF256_K_ENCODE_PREP = 0, NTC_GF256_K_ENCODE_MAC = 1, NTC_GF256_K_DECODE_PLAN = 2,
+       NTC_GF256_K_PLAN_ROWS = 3, NTC_GF256_K_DECODE_MAC = 4, NTC_GF256_K_BJ_OFFSETS = 5,
+       NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 };
+int  ntc_gf256_timing_log(ntc_gf256_engine* eng, uint32_t capacity);
+int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uint32_t* kinds,
+                           float* ms);
 
 /* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture). */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);

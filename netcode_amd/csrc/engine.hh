@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "netcode/gpu.h"
 
@@ -27,9 +28,14 @@ struct ntc_gf256_engine {
   void* row_ptr = nullptr;     // bit-sliced decode: input row address per plan position
   size_t row_ptr_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;
+  int plan_kind = NTC_GF256_PLAN_AUTO;
   // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
   bool timing = false;
   hipEvent_t mac_ev[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  // kernel timing log (ntc_gf256_timing_log): an event pair around every launch, in launch order
+  uint32_t tlog_cap = 0, tlog_n = 0;
+  std::vector<hipEvent_t> tlog_ev;     // 2 per entry
+  std::vector<uint32_t> tlog_kind;     // NTC_GF256_K_*
   // geometry of the last plan (decode_apply must match)
   uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
   // dense-code workspace (ntc_dense.hip): augmented matrices (ping-pong), panel trackers,
@@ -53,5 +59,31 @@ int hip_check(hipError_t e, const char* what);
 int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
 // Coefficient rows padded to the MAC kernels' row tile (ntc_gf256_coef_pitch).
 uint32_t tile_rp(uint32_t r);
+
+// Scope guard around one kernel launch: with the timing log on (and room left) records the
+// entry's start event before the launch and its end event when the scope closes, both on the
+// launch stream, so the pair brackets exactly that kernel in stream order.
+class KernelTimer {
+ public:
+  KernelTimer(ntc_gf256_engine* e, uint32_t kind, hipStream_t st) : e_(e), st_(st)
+  {
+    if (e_->tlog_n < e_->tlog_cap) {
+      slot_ = static_cast<int>(e_->tlog_n++);
+      e_->tlog_kind[slot_] = kind;
+      (void)hipEventRecord(e_->tlog_ev[2 * slot_], st_);
+    }
+  }
+  ~KernelTimer()
+  {
+    if (slot_ >= 0) (void)hipEventRecord(e_->tlog_ev[2 * slot_ + 1], st_);
+  }
+  KernelTimer(const KernelTimer&) = delete;
+  KernelTimer& operator=(const KernelTimer&) = delete;
+
+ private:
+  ntc_gf256_engine* e_;
+  hipStream_t st_;
+  int slot_ = -1;
+};
 
 }  // namespace ntcgpu

@@ -423,8 +423,11 @@ int ntc_gf256_dense_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, ui
   int rc = ensure_buf(&e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * k * pitch + 64, "hipMalloc dense coef");
   if (rc) return rc;
   // combine wants coef[g][i][j] (input-major): the transpose of mat[g][j][i]
-  hipLaunchKernelGGL(dn_transpose, dim3((k + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, r, k,
-                     pitch, mat, static_cast<uint8_t*>(e->dn_coef));
+  {
+    KernelTimer kt(e, NTC_GF256_K_DENSE, st);
+    hipLaunchKernelGGL(dn_transpose, dim3((k + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, r, k,
+                       pitch, mat, static_cast<uint8_t*>(e->dn_coef));
+  }
   if ((rc = hip_check(hipGetLastError(), "dn_transpose launch"))) return rc;
   return ntc_gf256_combine_batch(e, G, k, r, stride, src, static_cast<const uint8_t*>(e->dn_coef), rep, stream);
 }
@@ -442,19 +445,22 @@ int ntc_gf256_dense_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t n, ui
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint8_t* X;
   uint32_t np;
-  int rc = dense_invert(e, G, n, mat, st, &X, &np);
-  if (rc) return rc;
+  const uint32_t pitch = ntc_gf256_coef_pitch(n);
+  int rc;
+  {   // timing log: the inversion and the coefficient layout as one NTC_GF256_K_DENSE entry
+    KernelTimer kt(e, NTC_GF256_K_DENSE, st);
+    if ((rc = dense_invert(e, G, n, mat, st, &X, &np))) return rc;
   // M^-1 rows into the Y buffer (free after the last swap), then transposed into combine layout:
   // out[g][t] = sum_i inv[t][i] * rep[g][i]  ->  coef[g][i][t] = inv[t][i]
   uint8_t* invbuf = static_cast<uint8_t*>(X == e->dn_x ? e->dn_y : e->dn_x);
   hipLaunchKernelGGL(dn_gather_inv, dim3(n, G), dim3(256), 0, st, n, np, X,
                      static_cast<const uint32_t*>(e->dn_piv), static_cast<const uint8_t*>(e->dn_ok), invbuf);
   if ((rc = hip_check(hipGetLastError(), "dn_gather_inv launch"))) return rc;
-  const uint32_t pitch = ntc_gf256_coef_pitch(n);
   if ((rc = ensure_buf(&e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * n * pitch + 64, "hipMalloc dense coef"))) return rc;
   hipLaunchKernelGGL(dn_transpose, dim3((n + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, n, n,
                      pitch, invbuf, static_cast<uint8_t*>(e->dn_coef));
   if ((rc = hip_check(hipGetLastError(), "dn_transpose launch"))) return rc;
+  }
   if ((rc = ntc_gf256_combine_batch(e, G, n, n, stride, rep, static_cast<const uint8_t*>(e->dn_coef), out, stream))) return rc;
   return copy_ok(e, G, ok, st);
 }

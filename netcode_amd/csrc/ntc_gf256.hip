@@ -1875,9 +1875,12 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
       if (rc) return rc;
-      hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
-                         a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
-                         a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
+      {
+        KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
+        hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
+                           a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
+                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
+      }
       if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
       a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
     }
@@ -1889,6 +1892,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       if (rc) return rc;
       a.joff = static_cast<const uint32_t*>(e->joff);
       const uint64_t n4 = n / 4;
+      KernelTimer kt(e, NTC_GF256_K_BJ_OFFSETS, st);
       hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n4 + 255) / 256)), dim3(256), 0,
                          st, a.coef, a.rp, rt, a.ntiles, n4, static_cast<uint32_t*>(e->joff));
       if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
@@ -1924,7 +1928,10 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
-  hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, a);
+  {
+    KernelTimer kt(e, dec ? NTC_GF256_K_DECODE_MAC : NTC_GF256_K_ENCODE_MAC, st);
+    hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, a);
+  }
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][1], st);
   return hip_check(hipGetLastError(), what);
 }
@@ -2050,6 +2057,8 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   for (auto& pair : e->mac_ev)
     for (hipEvent_t ev : pair)
       if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->tlog_ev)
+    if (ev) (void)hipEventDestroy(ev);
   delete e;
 }
 
@@ -2082,6 +2091,54 @@ int ntc_gf256_set_mac_kind(ntc_gf256_engine* e, int kind)
   if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
   if (kind < NTC_GF256_MAC_AUTO || kind > NTC_GF256_MAC_BITSLICE) return fail(NTC_GPU_EINVAL, "unknown MAC kind");
   e->mac_kind = kind;
+  return NTC_GPU_OK;
+}
+
+int ntc_gf256_set_plan_kind(ntc_gf256_engine* e, int kind)
+{
+  if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
+  if (kind < NTC_GF256_PLAN_AUTO || kind > NTC_GF256_PLAN_BIG) return fail(NTC_GPU_EINVAL, "unknown plan kind");
+  e->plan_kind = kind;
+  return NTC_GPU_OK;
+}
+
+int ntc_gf256_timing_log(ntc_gf256_engine* e, uint32_t capacity)
+{
+  if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
+  (void)hipSetDevice(e->device);
+  // events of a previous log may still be pending on some stream: wait before reusing them
+  for (uint32_t i = 0; i < e->tlog_n; ++i) (void)hipEventSynchronize(e->tlog_ev[2 * i + 1]);
+  e->tlog_n = 0;
+  e->tlog_cap = 0;
+  if (2u * capacity > e->tlog_ev.size()) {
+    const size_t have = e->tlog_ev.size();
+    e->tlog_ev.resize(2u * capacity, nullptr);
+    for (size_t i = have; i < e->tlog_ev.size(); ++i) {
+      int rc = hip_check(hipEventCreate(&e->tlog_ev[i]), "hipEventCreate");
+      if (rc) {
+        e->tlog_ev.resize(i);
+        return rc;
+      }
+    }
+  }
+  e->tlog_kind.assign(capacity, NTC_GF256_K_OTHER);
+  e->tlog_cap = capacity;
+  return NTC_GPU_OK;
+}
+
+int ntc_gf256_timing_read(ntc_gf256_engine* e, uint32_t max, uint32_t* n, uint32_t* kinds, float* ms)
+{
+  if (!e || !n || (max && (!kinds || !ms))) return fail(NTC_GPU_EINVAL, "NULL argument");
+  *n = e->tlog_n;
+  const uint32_t cnt = e->tlog_n < max ? e->tlog_n : max;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    int rc = hip_check(hipEventSynchronize(e->tlog_ev[2 * i + 1]), "hipEventSynchronize");
+    if (rc) return rc;
+    if ((rc = hip_check(hipEventElapsedTime(&ms[i], e->tlog_ev[2 * i], e->tlog_ev[2 * i + 1]),
+                        "hipEventElapsedTime")))
+      return rc;
+    kinds[i] = e->tlog_kind[i];
+  }
   return NTC_GPU_OK;
 }
 
@@ -2127,7 +2184,10 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
     if (rc) return rc;
     p.coef = static_cast<uint8_t*>(e->enc_coef);
   }
-  hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
+  {
+    KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st);
+    hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
+  }
   if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
@@ -2145,12 +2205,16 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     return fail(NTC_GPU_EINVAL, "NULL argument");
   if (G == 0 || k == 0) return fail(NTC_GPU_EINVAL, "G and k must be > 0");
   if (r > kBigRows) return fail(NTC_GPU_EUNSUPPORTED, "r > 255 not supported by decode (w = 8 limit)");
-  // NTC_GF256_PLAN=big: decode_plan_big for every r (A/B and coverage of the big kernel)
-  static const bool force_big = [] {
+  // Plan kernel: the engine's plan kind (ntc_gf256_set_plan_kind); under AUTO the environment
+  // variable NTC_GF256_PLAN=lds|big may force one (A/B experiments, process-wide).
+  static const int env_plan = [] {
     const char* v = std::getenv("NTC_GF256_PLAN");
-    return v && !std::strcmp(v, "big");
+    if (v && !std::strcmp(v, "big")) return static_cast<int>(NTC_GF256_PLAN_BIG);
+    if (v && !std::strcmp(v, "lds")) return static_cast<int>(NTC_GF256_PLAN_LDS);
+    return static_cast<int>(NTC_GF256_PLAN_AUTO);
   }();
-  const bool big = r > static_cast<uint32_t>(kMaxPlanRows) || (force_big && r > 0);
+  const int kind = e && e->plan_kind != NTC_GF256_PLAN_AUTO ? e->plan_kind : env_plan;
+  const bool big = r > static_cast<uint32_t>(kMaxPlanRows) || (kind == NTC_GF256_PLAN_BIG && r > 0);
   if (big) offsets = false;                 // apply computes the bit-sliced offsets (bj_offsets)
   if (k > 65535) return fail(NTC_GPU_EUNSUPPORTED, "k > 65535");
   const uint32_t rp = tile_rp(r);
@@ -2174,16 +2238,14 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
   p.ablate = ablate;
-  // r <= 32: the register-resident plan (four generations per block); NTC_GF256_PLAN=lds selects
-  // the LDS Gauss-Jordan kernel instead (A/B only; r > 32 always uses it)
-  static const bool lds_plan = [] {
-    const char* v = std::getenv("NTC_GF256_PLAN");
-    return v && !std::strcmp(v, "lds");
-  }();
+  // r <= 32: the register-resident plan (four generations per block); PLAN_LDS selects the LDS
+  // Gauss-Jordan kernel instead (r > 32 always uses it)
+  const bool lds_plan = kind == NTC_GF256_PLAN_LDS;
   static const uint32_t ablate_w = [] {   // timing ablations of decode_plan_w (results wrong)
     const char* v = std::getenv("NTC_GF256_PLANW_ABLATE");
     return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
+  KernelTimer kt(e, NTC_GF256_K_DECODE_PLAN, static_cast<hipStream_t>(stream));
   if (big) {
     p.big_pitch = ((2 * r + 3) / 4) | 1u;
     p.big_rows = r;

@@ -102,6 +102,31 @@ class Engine:
         _native.check(self._L.ntc_gf256_set_mac_kind(self._h, Engine.MAC_KINDS[kind]),
                       "ntc_gf256_set_mac_kind")
 
+    PLAN_KINDS = {"auto": 0, "wave": 1, "lds": 2, "big": 3}
+
+    def set_plan_kind(self, kind: str = "auto"):
+        """Select the decode-plan kernel (ntc_gf256_set_plan_kind); results are identical."""
+        _native.check(self._L.ntc_gf256_set_plan_kind(self._h, Engine.PLAN_KINDS[kind]),
+                      "ntc_gf256_set_plan_kind")
+
+    KERNEL_KINDS = ("encode_prep", "encode_mac", "decode_plan", "plan_rows", "decode_mac",
+                    "bj_offsets", "dense", "other")
+
+    def timing_log(self, capacity: int):
+        """Bracket each of the next `capacity` kernel launches with HIP events (0 = off)."""
+        _native.check(self._L.ntc_gf256_timing_log(self._h, int(capacity)), "ntc_gf256_timing_log")
+
+    def timing_read(self, max_entries: int = 1 << 16):
+        """[(kernel kind name, ms)] of the logged launches, in launch order (waits for them)."""
+        import ctypes as C
+        kinds = (C.c_uint32 * max_entries)()
+        ms = (C.c_float * max_entries)()
+        n = C.c_uint32()
+        _native.check(self._L.ntc_gf256_timing_read(self._h, max_entries, C.byref(n),
+                                                     C.addressof(kinds), C.addressof(ms)),
+                      "ntc_gf256_timing_read")
+        return [(Engine.KERNEL_KINDS[kinds[i]], float(ms[i])) for i in range(min(n.value, max_entries))]
+
     def reserve(self, G: int, k: int, r: int):
         _native.check(self._L.ntc_gf256_reserve(self._h, G, k, r), "ntc_gf256_reserve")
 

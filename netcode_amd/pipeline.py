@@ -9,7 +9,8 @@ Chunk c runs on slot c % depth: H2D -> encode/decode kernels -> D2H, all in stre
 slot's buffers are reused only after its previous chunk's D2H has been issued behind them.
 Results are byte-identical to one device-resident call over the whole batch (tests/
 test_gpu_pipeline.py): generations are independent and every chunk keeps its generations' id
-bases.
+bases -- with no explicit bases, chunk generations g0..g1 get the whole-batch defaults g*k / g*r
+(u32 wraparound), exactly what one BatchEncoder call over all G generations uses.
 """
 from __future__ import annotations
 
@@ -17,12 +18,24 @@ import torch
 
 from .engine import BatchDecoder, BatchEncoder, Engine, EncodeResult, STATUS_BYTES
 
+_I16 = (torch.int16, torch.uint16)
+
 
 def _pinned(t: torch.Tensor, name: str):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
     if t.device.type != "cpu" or not t.is_pinned():
         raise ValueError(f"{name} must be a pinned host tensor (torch.Tensor.pin_memory())")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
+
+
+def _default_bases(g0: int, g1: int, per_gen: int, device) -> torch.Tensor:
+    """u32 id bases (g * per_gen) mod 2^32 for generations g0..g1-1, as an int32 device tensor
+    (the kernels' fallback when no base pointer is given is the same product in u32)."""
+    v = (torch.arange(g0, g1, dtype=torch.int64) * per_gen) & 0xFFFFFFFF
+    v = torch.where(v >= 2**31, v - 2**32, v)
+    return v.to(torch.int32).to(device, non_blocking=False)
 
 
 class HostPipeline:
@@ -56,14 +69,45 @@ class HostPipeline:
         for c, g0 in enumerate(range(0, G, self.chunk)):
             yield c % self.depth, g0, min(G, g0 + self.chunk)
 
-    def _check(self, G: int, **tensors):
-        for name, t in tensors.items():
-            _pinned(t, name)
-            if t.shape[0] != G:
-                raise ValueError(f"{name}: expected {G} generations, got {t.shape[0]}")
+    # expected (dtypes, trailing shape) of every host argument, by name
+    def _spec(self, name: str):
+        k, r, S = self.k, self.r, self.stride
+        u8 = (torch.uint8,)
+        return {"h_src": (u8, (k, S)), "h_rx": (u8, (k, S)), "h_rep": (u8, (r, S)),
+                "h_src_len": (_I16, (k,)), "h_rx_len": (_I16, (k,)), "h_rep_size": (_I16, (r,)),
+                "h_rep_len": (_I16, ()), "h_mask": (u8, (k,)), "h_rmask": (u8, (r,)),
+                "h_status": (u8, (STATUS_BYTES,))}[name]
 
-    def _ids(self, base, g0, g1):
-        return None if base is None else base[g0:g1]
+    def _check(self, G: int, **tensors):
+        """Every host tensor: pinned, contiguous, [G, ...] with this pipeline's k / r / stride and
+        the dtype the device side expects (copy_ would silently cast or broadcast otherwise)."""
+        for name, t in tensors.items():
+            if t is None:
+                continue
+            _pinned(t, name)
+            dtypes, tail = self._spec(name)
+            if t.dtype not in dtypes:
+                raise TypeError(f"{name} must have dtype {dtypes}, got {t.dtype}")
+            if tuple(t.shape) != (G,) + tail:
+                raise ValueError(f"{name} must have shape {(G,) + tail}, got {tuple(t.shape)}")
+
+    def _check_bases(self, G: int, **bases):
+        for name, t in bases.items():
+            if t is None:
+                continue
+            if t.device != self.device or t.dtype not in (torch.int32, torch.uint32) or \
+                    tuple(t.shape) != (G,) or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous int32/uint32 [{G}] tensor on {self.device}")
+
+    def _bases(self, G: int, sid_base, rid_base):
+        """Explicit bases, or the whole-batch defaults (built on the caller's current stream,
+        which every chunk stream waits for in _fork)."""
+        self._check_bases(G, sid_base=sid_base, rid_base=rid_base)
+        if sid_base is None:
+            sid_base = _default_bases(0, G, self.k, self.device)
+        if rid_base is None:
+            rid_base = _default_bases(0, G, self.r, self.device)
+        return sid_base, rid_base
 
     def _fork(self):
         # work the caller queued before this call (device id bases, earlier copies) comes first
@@ -76,12 +120,17 @@ class HostPipeline:
         for s in self.streams:
             cur.wait_stream(s)
 
-    def encode(self, h_src, h_src_len, h_rep, h_rep_size, sid_base=None, rid_base=None):
+    def encode(self, h_src, h_src_len, h_rep, h_rep_size, sid_base=None, rid_base=None,
+               h_rep_len=None):
         """h_src [G,k,stride] u8, h_src_len [G,k] i16 -> h_rep [G,r,stride] u8, h_rep_size [G,r]
-        i16 (pinned host tensors).  sid_base / rid_base: optional device u32 [G] id bases.
-        Asynchronous with respect to the host; the caller's current stream waits for all chunks."""
+        i16, optionally h_rep_len [G] i16 (repair symbol length = max source length, what a repair
+        packet's header carries) -- pinned host tensors.  sid_base / rid_base: optional device u32
+        [G] id bases.  Asynchronous with respect to the host; the caller's current stream waits
+        for all chunks."""
         G = h_src.shape[0]
-        self._check(G, h_src=h_src, h_src_len=h_src_len, h_rep=h_rep, h_rep_size=h_rep_size)
+        self._check(G, h_src=h_src, h_src_len=h_src_len, h_rep=h_rep, h_rep_size=h_rep_size,
+                    h_rep_len=h_rep_len)
+        sid_base, rid_base = self._bases(G, sid_base, rid_base)
         self._fork()
         for s, g0, g1 in self._chunks(G):
             n = g1 - g0
@@ -90,19 +139,23 @@ class HostPipeline:
                 src.copy_(h_src[g0:g1], non_blocking=True)
                 ln.copy_(h_src_len[g0:g1], non_blocking=True)
                 o = EncodeResult(out.repairs[:n], out.encoded_size[:n], out.symbol_len[:n])
-                self.enc[s](src, ln, self._ids(sid_base, g0, g1), self._ids(rid_base, g0, g1), o)
+                self.enc[s](src, ln, sid_base[g0:g1], rid_base[g0:g1], o)
                 h_rep[g0:g1].copy_(o.repairs, non_blocking=True)
                 h_rep_size[g0:g1].copy_(o.encoded_size, non_blocking=True)
+                if h_rep_len is not None:
+                    h_rep_len[g0:g1].copy_(o.symbol_len, non_blocking=True)
         self._join()
 
     def decode(self, h_rx, h_rx_len, h_mask, h_rep, h_rep_size, h_rmask, h_status,
                sid_base=None, rid_base=None):
         """In-place decode of host-resident generations: received sources h_rx [G,k,stride]
-        (lost slots are overwritten with the recovered sources), h_rx_len / h_mask [G,k], repairs
-        h_rep [G,r,stride] / h_rep_size / h_rmask [G,r], status out h_status [G,12] u8."""
+        (lost slots are overwritten with the recovered sources, and their h_rx_len entries with
+        the decoded sizes), h_rx_len / h_mask [G,k], repairs h_rep [G,r,stride] / h_rep_size /
+        h_rmask [G,r], status out h_status [G,12] u8."""
         G = h_rx.shape[0]
         self._check(G, h_rx=h_rx, h_rx_len=h_rx_len, h_mask=h_mask, h_rep=h_rep,
                     h_rep_size=h_rep_size, h_rmask=h_rmask, h_status=h_status)
+        sid_base, rid_base = self._bases(G, sid_base, rid_base)
         self._fork()
         for s, g0, g1 in self._chunks(G):
             n = g1 - g0
@@ -113,9 +166,9 @@ class HostPipeline:
                 for d, h in ((rx, h_rx), (ln, h_rx_len), (mk, h_mask), (rep, h_rep), (rsz, h_rep_size),
                              (rmk, h_rmask)):
                     d.copy_(h[g0:g1], non_blocking=True)
-                self.dec[s](rx, ln, mk, rep, rsz, rmk, self._ids(sid_base, g0, g1),
-                            self._ids(rid_base, g0, g1), st)
+                self.dec[s](rx, ln, mk, rep, rsz, rmk, sid_base[g0:g1], rid_base[g0:g1], st)
                 h_rx[g0:g1].copy_(rx, non_blocking=True)
+                h_rx_len[g0:g1].copy_(ln, non_blocking=True)
                 h_status[g0:g1].copy_(st, non_blocking=True)
         self._join()
 
@@ -123,11 +176,12 @@ class HostPipeline:
                       h_status, sid_base=None, rid_base=None):
         """Loopback of one batch (bench.py's host-resident rate): per chunk, sources H2D -> encode
         -> repairs D2H to h_rep, then received sources H2D -> decode with the chunk's repairs
-        still on the device -> recovered sources and status D2H.  Same results as encode() then
-        decode() with h_rep as the decoder's repairs."""
+        still on the device -> recovered sources, their decoded sizes and status D2H.  Same
+        results as encode() then decode() with h_rep as the decoder's repairs."""
         G = h_src.shape[0]
         self._check(G, h_src=h_src, h_src_len=h_src_len, h_rep=h_rep, h_rep_size=h_rep_size,
                     h_rx=h_rx, h_rx_len=h_rx_len, h_mask=h_mask, h_rmask=h_rmask, h_status=h_status)
+        sid_base, rid_base = self._bases(G, sid_base, rid_base)
         self._fork()
         for s, g0, g1 in self._chunks(G):
             n = g1 - g0
@@ -135,7 +189,7 @@ class HostPipeline:
                 buf, ln, mk, rmk = self.d_src[s][:n], self.d_len[s][:n], self.d_mask[s][:n], self.d_rmask[s][:n]
                 out, st = self.d_out[s], self.d_status[s][:n]
                 o = EncodeResult(out.repairs[:n], out.encoded_size[:n], out.symbol_len[:n])
-                sid, rid = self._ids(sid_base, g0, g1), self._ids(rid_base, g0, g1)
+                sid, rid = sid_base[g0:g1], rid_base[g0:g1]
                 buf.copy_(h_src[g0:g1], non_blocking=True)
                 ln.copy_(h_src_len[g0:g1], non_blocking=True)
                 self.enc[s](buf, ln, sid, rid, o)
@@ -146,5 +200,6 @@ class HostPipeline:
                     d.copy_(h[g0:g1], non_blocking=True)
                 self.dec[s](buf, ln, mk, o.repairs, o.encoded_size, rmk, sid, rid, st)
                 h_rx[g0:g1].copy_(buf, non_blocking=True)
+                h_rx_len[g0:g1].copy_(ln, non_blocking=True)
                 h_status[g0:g1].copy_(st, non_blocking=True)
         self._join()

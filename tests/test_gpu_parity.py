@@ -177,6 +177,55 @@ def test_decode_parity(gpu, mac, oracle, G, k, r, S, stride, kind, param, ragged
     assert (out[ok] == src[ok]).all()
 
 
+@pytest.mark.parametrize("plan", ["wave", "lds", "big"])
+@pytest.mark.parametrize("G,k,r,S,stride,kind,param,ragged", DECODE_CASES)
+def test_decode_parity_plan_kinds(gpu, oracle, plan, G, k, r, S, stride, kind, param, ragged):
+    """Every decode-plan kernel (ntc_gf256_set_plan_kind) on every decode case: the register
+    wave plan (r <= 32, else the LDS plan), the LDS wave plan (r <= 64) and the workgroup plan
+    with rank screening (decode_plan_big, forced for small r too) give the oracle's bytes,
+    sizes and status."""
+    from netcode_amd.engine import Engine
+    eng = Engine.get(gpu)
+    eng.set_plan_kind(plan)
+    try:
+        test_decode_parity(gpu, "auto", oracle, G, k, r, S, stride, kind, param, ragged)
+    finally:
+        eng.set_plan_kind("auto")
+
+
+def test_kernel_timing_log(gpu):
+    """ntc_gf256_timing_log / timing_read (bench.py's in-step kernel clock): one entry per launch
+    in launch order, positive durations whose sum fits inside the calls' wall time."""
+    import torch
+    from netcode_amd import BatchDecoder, BatchEncoder
+    from netcode_amd.engine import Engine
+    G, k, r, S = 64, 64, 16, 4096
+    src, lens = make_sources(G, k, S, S, seed=3)
+    s_t, l_t = dev(src, gpu), dev(lens, gpu)
+    eng = Engine.get(gpu)
+    smask = dev(loss_exact_m(G, k, 8, 4), gpu)
+    rmask = torch.ones((G, r), dtype=torch.uint8, device=gpu)
+    enc = BatchEncoder(k, r, gpu)(s_t, l_t)
+    torch.cuda.synchronize(gpu)
+    eng.timing_log(64)
+    try:
+        s = torch.cuda.current_stream(gpu)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(s)
+        enc = BatchEncoder(k, r, gpu)(s_t, l_t, out=enc)
+        BatchDecoder(k, r, gpu)(s_t, l_t, smask, enc.repairs, enc.encoded_size, rmask)
+        ev[1].record(s)
+        log = eng.timing_read()
+        torch.cuda.synchronize(gpu)
+        names = [n for n, _ in log]
+        assert names[:2] == ["encode_prep", "encode_mac"]
+        assert "decode_plan" in names and names[-1] == "decode_mac"
+        assert all(ms > 0 for _, ms in log)
+        assert sum(ms for _, ms in log) <= ev[0].elapsed_time(ev[1]) + 1e-3
+    finally:
+        eng.timing_log(0)
+
+
 def test_full_size_round_trip_config3(gpu, oracle):
     """Config 3 at BASELINE size (G=4096, k=128, r=32, 4 KiB, m=32).  Size-independent checks:
     every generation the plan reports decoded reproduces its sources exactly, and the per-

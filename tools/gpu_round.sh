@@ -4,7 +4,7 @@
 set -e
 TAG=${1:-run}
 mkdir -p gpurun_out/$TAG
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/$TAG/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/$TAG/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/$TAG/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/$TAG/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/$TAG/pytest_gpu.log
 timeout -k 10 300 python bench.py > gpurun_out/$TAG/bench.log 2>&1 || { tail -20 gpurun_out/$TAG/bench.log; exit 1; }
 tail -1 gpurun_out/$TAG/bench.log

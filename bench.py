@@ -115,7 +115,7 @@ class Workload:
         good = bool((self.rx[ok] == self.src[ok]).all())
         lossy = st["nb_missing"] > 0            # m = 0 (mixed runs): "nothing missing" is right
         allowed = np.where(lossy, np.isin(st["state"], (0, 3)), st["state"] == 1)
-        good = good and bool(allowed.all()) and dec[lossy].mean() >= 0.9
+        good = bool(good and allowed.all() and dec[lossy].mean() >= 0.9)
         m = st["nb_missing"].astype(np.int64)[dec]
         # decode MAC per decoded generation: reads (k - m) received sources + m repairs, writes m
         dec_bytes = int(((self.k + m) * self.S).sum())

@@ -60,38 +60,78 @@ def build(force: bool = False, verbose: bool = True) -> list[str]:
 # compiled unmodified against our headers and libntc.so.  Outputs go to tests/_build/ (git-ignored,
 # shipped to the GPU box with the tree).
 REF = "/root/reference"
+OUT_DIR = os.path.join(ROOT, "tests", "_build")
+# name: (sources, is_reference_program).  Reference programs are compiled unmodified, straight
+# from /root/reference; every netcode/ header they include resolves to include/ (this repo).
 CPP_CHECKS = {
-    "cpp_surface_test": ("tests/cpp/cpp_surface_test.cc", False),
-    "ref_cpp_basic": (REF + "/examples/basic/cpp_basic.cc", True),
-    "ref_c_basic": (REF + "/examples/basic/c_basic.c", True),
-    "ref_end_to_end": (REF + "/tests/end_to_end.cc", True),
+    "cpp_surface_test": (["tests/cpp/cpp_surface_test.cc"], False),
+    "ref_cpp_basic": ([REF + "/examples/basic/cpp_basic.cc"], True),
+    "ref_c_basic": ([REF + "/examples/basic/c_basic.c"], True),
+    "ref_end_to_end": ([REF + "/tests/end_to_end.cc"], True),
+    # ctest EndToEnd-MT (tests/CMakeLists.txt:31): encoder and decoder on two threads
+    "ref_end_to_end_mt": ([REF + "/tests/end_to_end_mt.cc"], True),
+    # the reference's Catch unit tests (ctest UnitTests, tests/CMakeLists.txt:1-29) that compile
+    # against this repo's headers; linked with the reference's Catch main (tests/tests.cc)
+    "ref_unit_public": ([REF + "/tests/netcode/test_packet.cc", REF + "/tests/netcode/c/test_data.cc",
+                         REF + "/tests/netcode/c/test_decoder.cc"], True),
 }
 
 
+def _ref_include_dir() -> str:
+    """An include root exposing ONLY the reference's test helpers (tests/, tools/ -- e.g.
+    tests/netcode/launch.hh, tools/loss/burst.hh), never its netcode/ library headers: a header
+    this repo lacked must fail the build, not silently resolve to the reference's."""
+    d = os.path.join(OUT_DIR, "refinc")
+    os.makedirs(d, exist_ok=True)
+    for sub in ("tests", "tools"):
+        link = os.path.join(d, sub)
+        if not os.path.islink(link):
+            os.symlink(os.path.join(REF, sub), link)
+    return d
+
+
+def _catch_main(verbose: bool) -> str:
+    """The reference's Catch main (tests/tests.cc), compiled once (catch.hpp is large)."""
+    obj = os.path.join(OUT_DIR, "ref_catch_main.o")
+    src = os.path.join(REF, "tests", "tests.cc")
+    if not os.path.exists(obj) or os.path.getmtime(obj) < os.path.getmtime(src):
+        cmd = ["g++", "-std=c++11", "-O1", "-DCATCH_CONFIG_NO_POSIX_SIGNALS", "-I", REF + "/ext",
+               "-c", "-o", obj, src]
+        if verbose:
+            print("[netcode_amd.build]", " ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    return obj
+
+
 def build_cpp_checks(verbose: bool = True) -> list[str]:
-    out_dir = os.path.join(ROOT, "tests", "_build")
-    os.makedirs(out_dir, exist_ok=True)
+    os.makedirs(OUT_DIR, exist_ok=True)
     lib_dir = HERE
     built = []
-    for name, (src, is_ref) in CPP_CHECKS.items():
-        src_p = src if os.path.isabs(src) else os.path.join(ROOT, src)
-        if not os.path.exists(src_p):
+    for name, (srcs, is_ref) in CPP_CHECKS.items():
+        srcs_p = [s if os.path.isabs(s) else os.path.join(ROOT, s) for s in srcs]
+        if not all(os.path.exists(s) for s in srcs_p):
             continue
-        out = os.path.join(out_dir, name)
-        deps = [src_p, os.path.join(HERE, "libntc.so")]
+        out = os.path.join(OUT_DIR, name)
+        deps = srcs_p + [os.path.join(HERE, "libntc.so"), os.path.abspath(__file__)]
         for d in ("include/netcode", "include/netcode/detail", "include/netcode/c"):
             dd = os.path.join(ROOT, d)
             deps += [os.path.join(dd, f) for f in os.listdir(dd)]
         if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps if os.path.exists(d)):
             built.append(out)
             continue
-        c = src_p.endswith(".c")
-        cmd = ["gcc" if c else "g++", "-std=c11" if c else "-std=c++11", "-O2", "-Wall",
-               "-I", os.path.join(ROOT, "include")]
+        c = srcs_p[0].endswith(".c")
+        catch = name.startswith("ref_unit")
+        cmd = ["gcc" if c else "g++", "-std=c11" if c else "-std=c++11", "-O1" if catch else "-O2",
+               "-Wall", "-I", os.path.join(ROOT, "include")]
         if is_ref:
-            cmd += ["-I", REF]          # only for the reference's own test helpers (tools/loss)
-        cmd += ["-o", out, src_p, "-L", lib_dir, "-lntc", "-lntc_gf256",
-                "-Wl,-rpath," + os.path.relpath(lib_dir, out_dir).join(["$ORIGIN/", ""])]
+            cmd += ["-I", _ref_include_dir()]
+        if catch:
+            cmd += ["-DCATCH_CONFIG_NO_POSIX_SIGNALS", "-I", REF + "/ext"]
+        cmd += ["-o", out] + srcs_p
+        if catch:
+            cmd.append(_catch_main(verbose))
+        cmd += ["-L", lib_dir, "-lntc", "-lntc_gf256", "-pthread",
+                "-Wl,-rpath," + os.path.relpath(lib_dir, OUT_DIR).join(["$ORIGIN/", ""])]
         if verbose:
             print("[netcode_amd.build]", " ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

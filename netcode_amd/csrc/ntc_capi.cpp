@@ -59,7 +59,9 @@ struct Align16 {
 using bytes = std::vector<uint8_t, Align16<uint8_t>>;
 
 // ---------------------------------------------------------------------- device engine ----
-// One engine + stream + staging per process (objects are not thread-safe, like the reference).
+// One engine + stream + staging per process.  Encoders and decoders are not thread-safe (like the
+// reference), but distinct objects may live on distinct threads (tests/end_to_end_mt.cc runs an
+// encoder and a decoder on two threads), so every use of the shared staging holds mu_.
 class Device {
  public:
   static Device& get()
@@ -84,6 +86,7 @@ class Device {
                     size_t rows, const uint32_t* coef /*[n][rows]*/, size_t out_len,
                     uint8_t* const* out)
   {
+    std::lock_guard<std::mutex> lock(mu_);
     size_t mx = out_len;
     for (size_t i = 0; i < n; ++i) mx = std::max<size_t>(mx, lens[i]);
     const size_t stride = std::max<size_t>(16, (mx + 15) / 16 * 16);
@@ -120,6 +123,7 @@ class Device {
   template <typename Fill, typename Sink>
   void combine_generations(uint32_t w, size_t G, size_t k, size_t stride, Fill fill, Sink sink)
   {
+    std::lock_guard<std::mutex> lock(mu_);
     const uint32_t pitch = w == 8 ? ntc_gf256_coef_pitch(1) : 4u;
     grow(G * k * stride, G * k * pitch, G * stride);
     std::memset(h_coef_, 0, G * k * pitch);
@@ -195,6 +199,7 @@ class Device {
     ++launches_;
   }
 
+  std::mutex mu_;
   ntc_gf256_engine* eng_ = nullptr;
   hipStream_t stream_ = nullptr;
   std::string err_;

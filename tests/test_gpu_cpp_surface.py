@@ -4,8 +4,11 @@
   handler exceptions, setters, and the tests/end_to_end.cc loop over 1000 packets, whose counters
   must equal the reference's golden counters (tests/golden/kat.json).
 * The reference's own programs compiled unmodified against our headers (built in the container
-  that holds the reference; skipped when absent): examples/basic/cpp_basic.cc, c_basic.c and
-  tests/end_to_end.cc, whose printed counters must equal the same golden values.
+  that holds the reference; skipped when absent): examples/basic/cpp_basic.cc, c_basic.c,
+  tests/end_to_end.cc (ctest EndToEnd, and at 10000 packets), whose printed counters must equal
+  the same golden values, tests/end_to_end_mt.cc (ctest EndToEnd-MT: encoder and decoder on two
+  threads), and the reference's Catch unit tests that compile against this repo's headers
+  (ctest UnitTests subset; netcode_amd/build.py CPP_CHECKS lists them).
 """
 import json
 import os
@@ -48,12 +51,15 @@ def test_reference_c_basic(gpu):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-def test_reference_end_to_end(gpu):
-    r = _run("ref_end_to_end", 1000)
+@pytest.mark.parametrize("n", [1000, 10000])
+def test_reference_end_to_end(gpu, n):
+    """ctest `EndToEnd end_to_end 1000` (tests/CMakeLists.txt:30) and the 10000-packet run: the
+    reference's own driver against libntc.so reproduces the SURVEY §6 golden counters."""
+    r = _run("ref_end_to_end", n, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     out = r.stdout.replace("\r", "\n")
     field = lambda k: int(re.search(rf"^{k} (\d+)$", out, re.M).group(1))
-    want = KAT["end_to_end"]["1000"]
+    want = KAT["end_to_end"][str(n)]
     assert field("Sent") == want["sent"]
     assert field("Lost") == want["lost"]
     assert field("Handled data") == want["handled_data"]
@@ -61,3 +67,22 @@ def test_reference_end_to_end(gpu):
     assert field("Received sources") == want["received_sources"]
     assert field("Useless repairs") == want["useless_repairs"]
     assert field("Decoded") == want["decoded"]
+
+
+def test_reference_end_to_end_mt(gpu):
+    """ctest `EndToEnd-MT end_to_end_mt 2` (tests/CMakeLists.txt:31): an encoder thread and a
+    decoder thread exchanging packets through lossy queues for 2 s.  The in-order data handler
+    throws (and the program aborts) on any out-of-order or corrupted delivery."""
+    r = _run("ref_end_to_end_mt", 2, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    handled = int(re.search(r"^Handled data (\d+)$", r.stdout, re.M).group(1))
+    sent = int(re.search(r"^Sent (\d+)$", r.stdout, re.M).group(1))
+    assert 0 < handled <= sent
+
+
+def test_reference_unit_tests_public(gpu):
+    """The reference's Catch tests that need only the public surface: tests/netcode/test_packet.cc
+    (ntc::packet), tests/netcode/c/test_data.cc and tests/netcode/c/test_decoder.cc (C ABI)."""
+    r = _run("ref_unit_public", timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "All tests passed" in r.stdout, r.stdout

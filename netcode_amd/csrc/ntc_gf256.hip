@@ -358,6 +358,9 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
 // matrix.  Per (source, row) that is 15 full-rate VALU ops for 32 bytes plus 4 scalar ops,
 // against 24 half-rate v_perm + 12 XOR for the byte-domain kernel.
 #include "gf_bitslice_chain.inc"
+// The shared-table variant (one dispatch per row, VGPR-relative accumulators; the GX kernels):
+// tools/gen_bitslice_gidx.py.
+#include "gf_bitslice_gidx.inc"
 
 // Delta swap of the `mask` bit groups of b with the groups `sh` bits higher in a: two shifts and
 // two bit-field inserts (v_bfi_b32 / v_bitop3), 4 VALU.
@@ -481,11 +484,15 @@ __device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, ui
 // 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain,
 // 16 every source uses source 0's jump offsets (scalar-cache-resident), 32 every generation reads
 // generation 0's sources (L2-resident), 64 no source DMAs at all (the ring holds stale bytes).
-template <int R, int RT, bool DEC, int ABL = 0>
+// GX: the shared-table chain (gf_bitslice_gidx.inc): a.joff holds, per (generation, source,
+// 8-row tile), 8 u16 block offsets (kGxOff[c] of the tile's rows) instead of the nibble-site
+// jump offsets; R must be 8 (fewer rows carry c = 0, which the chain skips).
+template <int R, int RT, bool DEC, int ABL = 0, bool GX = false>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
                                             const uint8_t* ring_p, uint32_t ring)
 {
+  static_assert(!GX || R == 8, "the shared-table chain works on 8-row tiles");
   const size_t stride = a.stride;
   const uint32_t k = a.k;
   const uint32_t c0 = cc * 2048u + lane * 16u, c1 = c0 + 1024u;
@@ -493,9 +500,11 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   const uint32_t x0 = v0 ? c0 : 0u, x1 = v1 ? c1 : 0u;  // invalid pieces read column 0 (unused)
   const uint8_t* base0 = a.in0 + static_cast<size_t>((ABL & 32) ? 0u : g) * k * stride;
   const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
-  const uint32_t jstep = a.ntiles * 2u * RT;
-  const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * (2u * RT);
-  constexpr int NJ = R == 16 ? 2 : 1;     // u32x16 offset vectors per source
+  constexpr uint32_t kOffDw = GX ? 4u : 2u * RT;   // offset dwords per (source, tile)
+  const uint32_t jstep = a.ntiles * kOffDw;
+  const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * kOffDw;
+  constexpr int NJ = R == 16 ? 2 : 1;     // offset vectors per source
+  using OffV = typename std::conditional<GX, u32x4, u32x16>::type;
   // Offsets and row addresses are loaded with ordinary uniform loads through the constant address
   // space (s_load, waits placed by the compiler).  Decode reads each input row's address from the
   // plan_rows table (padded by kBjRing entries, so the prefetches past position k-1 need no
@@ -514,6 +523,9 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   for (int j = 0; j < R; ++j)
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[j][p] = 0;
+  u32x8 A[GX ? R : 1];          // GX: the accumulators as register blocks pinned by the chain
+#pragma unroll
+  for (int j = 0; j < (GX ? R : 1); ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
 
   // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait counts are constant);
   // source 0 read into registers.  Steady state at iteration i: source i in registers, the LDS
@@ -526,13 +538,13 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   // row of source i + kBjRing - 1, the refill of iteration i (decode: loaded one iteration ahead)
   const uint8_t* nrow = row_at(kBjRing - 1);
   const uint32_t* jp = jrow;                           // offsets of source min(i + 1, k - 1)
-  u32x16 on[NJ];
+  OffV on[NJ];
 #pragma unroll
-  for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jrow + 16 * h);
+  for (int h = 0; h < NJ; ++h) on[h] = const_load<OffV>(jrow + 16 * h);
   auto next_offsets = [&](uint32_t i) {
     if constexpr (!(ABL & 16)) jp += (i + 1 < k) ? jstep : 0u;
 #pragma unroll
-    for (int h = 0; h < NJ; ++h) on[h] = const_load<u32x16>(jp + 16 * h);
+    for (int h = 0; h < NJ; ++h) on[h] = const_load<OffV>(jp + 16 * h);
   };
   uint32_t ycur[8];
   if constexpr (!kBjLateRead) {
@@ -540,7 +552,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     ring_read(ring_p, lane, ycur);
   }
   for (uint32_t i = 0; i < k; ++i) {
-    u32x16 o[NJ];
+    OffV o[NJ];
 #pragma unroll
     for (int h = 0; h < NJ; ++h) o[h] = on[h];
     uint32_t Y[kBjPlanes];
@@ -576,6 +588,12 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
       for (int n = 8; n < kBjPlanes; ++n) Y[n] = Y[n & 7] + n;
     }
+    if constexpr (GX) {
+      const uint64_t P0 = (static_cast<uint64_t>(o[0][1]) << 32) | o[0][0];   // rows 0-3
+      const uint64_t P1 = (static_cast<uint64_t>(o[0][3]) << 32) | o[0][2];   // rows 4-7
+      asm volatile(NTC_GX_CHAIN : NTC_GX_OUTS(A) : NTC_GX_INS(Y, P0, P1) : NTC_GX_CLOBBERS);
+      continue;
+    } else {
     uint32_t O[16 * NJ];
 #pragma unroll
     for (int s = 0; s < 16 * NJ; ++s) O[s] = o[s >> 4][s & 15];
@@ -601,9 +619,16 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     } else {
       asm volatile(NTC_BJ_CHAIN_R4 : NTC_BJ_OUTS_R4(acc) : NTC_BJ_INS_R4(Y, O) : NTC_BJ_CLOBBERS);
     }
+    }
   }
   // Drain the clamped trailing DMAs before the wave's LDS can be handed to another block.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (GX) {
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) acc[j][p] = A[j][p];
+  }
 
   const uint32_t row0 = tile * RT;
 #pragma unroll
@@ -630,7 +655,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #endif
 constexpr int kBjWaves = NTC_BJ_WPB;     // waves (independent tasks) per workgroup; tuning builds
 
-template <int RT, bool DEC, int ABL = 0>
+template <int RT, bool DEC, int ABL = 0, bool GX = false>
 #ifndef NTC_BJ_WAVES_PER_EU
 #define NTC_BJ_WAVES_PER_EU 1
 #endif
@@ -660,8 +685,33 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_
       return;
     }
   }
+  if constexpr (GX) {
+    mac_tile_bj<8, RT, DEC, ABL, true>(a, g, tile, nrows, cc, lane, ring_p, ring);
+    return;
+  }
   if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
   else mac_tile_bj<4, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
+}
+
+// Shared-table chain offsets: per (generation, source, 8-row tile) the 8 rows' kGxOff[c] as u16,
+// from the coefficient bytes coef[g][i][rp] (rows >= rp read as 0).  One thread per 16-byte entry.
+__global__ __launch_bounds__(256) void gx_offsets(const uint8_t* __restrict__ coef, uint32_t rp,
+                                                  uint32_t ntiles, uint64_t total,
+                                                  uint32_t* __restrict__ gxo)
+{
+  const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (idx >= total) return;
+  const uint32_t tile = static_cast<uint32_t>(idx % ntiles);
+  const uint64_t gi = idx / ntiles;
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t j0 = tile * 8u + 2u * q;
+    const uint32_t c0 = j0 < rp ? coef[gi * rp + j0] : 0u;
+    const uint32_t c1 = j0 + 1 < rp ? coef[gi * rp + j0 + 1] : 0u;
+    w[q] = static_cast<uint32_t>(kGxOff[c0]) | (static_cast<uint32_t>(kGxOff[c1]) << 16);
+  }
+  reinterpret_cast<uint4*>(gxo)[idx] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // Input row address of every plan position for the bit-sliced decode MAC: position i < k reads
@@ -1852,6 +1902,16 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
   return pieces * 100 >= spans * 128 * 70;
 }
 
+// NTC_GF256_BJ_GX=1: the bit-sliced MAC runs the shared-table chain (gf_bitslice_gidx.inc).
+bool gx_chain()
+{
+  static const bool gx = [] {
+    const char* v = std::getenv("NTC_GF256_BJ_GX");
+    return v && std::atoi(v) == 1;
+  }();
+  return gx;
+}
+
 // Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
 // `offsets_ready`: the bit-sliced jump offsets for 8-row tiles are already in e->joff (encode_prep).
 int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what,
@@ -1860,7 +1920,37 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   mac_fn fn;
   uint32_t rowtile = 32, span;
   uint64_t blk_align = 1;
-  if (use_bitslice(e, a.stride)) {
+  if (use_bitslice(e, a.stride) && gx_chain()) {
+    // shared-table chain: block offsets from the coefficient bytes (gx_offsets), 8-row tiles
+    rowtile = 8;
+    span = 2048;
+    blk_align = 8;
+    fn = dec ? gf_mac_bj<8, true, 0, true> : gf_mac_bj<8, false, 0, true>;
+    a.ntiles = (a.rows + 7) / 8;
+    if (dec) {
+      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
+      int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
+      if (rc) return rc;
+      {
+        KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
+        hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
+                           a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
+                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
+      }
+      if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
+      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
+    }
+    const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles;
+    int rc = ensure_buf(&e->joff, &e->joff_cap, n * 16, "hipMalloc gx offsets");
+    if (rc) return rc;
+    a.joff = static_cast<const uint32_t*>(e->joff);
+    {
+      KernelTimer kt(e, NTC_GF256_K_BJ_OFFSETS, st);
+      hipLaunchKernelGGL(gx_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
+                         a.coef, a.rp, a.ntiles, n, static_cast<uint32_t*>(e->joff));
+    }
+    if ((rc = hip_check(hipGetLastError(), "gx_offsets launch"))) return rc;
+  } else if (use_bitslice(e, a.stride)) {
     static const uint32_t rt = [] {
       const char* v = std::getenv("NTC_GF256_BJ_ROWS");      // 8 | 16 (tuning experiments)
       return (v && std::atoi(v) == 16) ? 16u : 8u;
@@ -2172,7 +2262,7 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
     const char* v = std::getenv("NTC_GF256_BJ_ROWS");
     return v && std::atoi(v) == 16;
   }();
-  const bool fused = use_bitslice(e, stride) && !rows16;
+  const bool fused = use_bitslice(e, stride) && !rows16 && !gx_chain();
   if (fused) {
     p.ntiles = (r + 7u) / 8u;
     const size_t n = static_cast<size_t>(G) * k * p.ntiles * 16u;
@@ -2279,7 +2369,7 @@ static bool bitslice_rt8(const ntc_gf256_engine* e, uint32_t stride)
     const char* v = std::getenv("NTC_GF256_BJ_ROWS");
     return v && std::atoi(v) == 16;
   }();
-  return use_bitslice(e, stride) && !rows16;
+  return use_bitslice(e, stride) && !rows16 && !gx_chain();
 }
 
 int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,

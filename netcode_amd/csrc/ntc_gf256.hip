@@ -484,10 +484,11 @@ __device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, ui
 // 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain,
 // 16 every source uses source 0's jump offsets (scalar-cache-resident), 32 every generation reads
 // generation 0's sources (L2-resident), 64 no source DMAs at all (the ring holds stale bytes).
-// GX: the shared-table chain (gf_bitslice_gidx.inc): a.joff holds, per (generation, source,
-// 8-row tile), 8 u16 block offsets (kGxOff[c] of the tile's rows) instead of the nibble-site
-// jump offsets; R must be 8 (fewer rows carry c = 0, which the chain skips).
-template <int R, int RT, bool DEC, int ABL = 0, bool GX = false>
+// GX: the shared-table chains (gf_bitslice_gidx.inc).  GX = 1: a.joff holds, per (generation,
+// source, 8-row tile), 8 u16 block offsets (kGxOff[c] of the tile's rows) instead of the nibble-
+// site jump offsets.  GX = 2: the chain reads the coefficient bytes a.coef [G][k][rp] directly
+// (8 rows = one u64 per source).  R must be 8 (fewer rows carry c = 0, which the chains skip).
+template <int R, int RT, bool DEC, int ABL = 0, int GX = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
                                             const uint8_t* ring_p, uint32_t ring)
@@ -500,11 +501,16 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   const uint32_t x0 = v0 ? c0 : 0u, x1 = v1 ? c1 : 0u;  // invalid pieces read column 0 (unused)
   const uint8_t* base0 = a.in0 + static_cast<size_t>((ABL & 32) ? 0u : g) * k * stride;
   const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
-  constexpr uint32_t kOffDw = GX ? 4u : 2u * RT;   // offset dwords per (source, tile)
-  const uint32_t jstep = a.ntiles * kOffDw;
-  const uint32_t* jrow = a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * kOffDw;
+  constexpr uint32_t kOffDw = GX == 1 ? 4u : 2u * RT;   // offset dwords per (source, tile)
+  // GX = 2: one source's coefficient row is rp bytes (rp % 4 == 0); the tile's 8 start at 8*tile
+  const uint32_t jstep = GX == 2 ? a.rp / 4u : a.ntiles * kOffDw;
+  const uint32_t* jrow = GX == 2
+      ? reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * 8u)
+      : a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * kOffDw;
   constexpr int NJ = R == 16 ? 2 : 1;     // offset vectors per source
-  using OffV = typename std::conditional<GX, u32x4, u32x16>::type;
+  using OffV = typename std::conditional<GX == 1, u32x4,
+               typename std::conditional<GX == 2, u32x2, u32x16>::type>::type;
+  const uint64_t pmask = a.rp >= 8 ? ~0ull : 0xFFFFFFFFull;   // rp = 4: bytes 4-7 = next source
   // Offsets and row addresses are loaded with ordinary uniform loads through the constant address
   // space (s_load, waits placed by the compiler).  Decode reads each input row's address from the
   // plan_rows table (padded by kBjRing entries, so the prefetches past position k-1 need no
@@ -526,6 +532,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   u32x8 A[GX ? R : 1];          // GX: the accumulators as register blocks pinned by the chain
 #pragma unroll
   for (int j = 0; j < (GX ? R : 1); ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
+  (void)pmask;
 
   // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait counts are constant);
   // source 0 read into registers.  Steady state at iteration i: source i in registers, the LDS
@@ -588,10 +595,14 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
       for (int n = 8; n < kBjPlanes; ++n) Y[n] = Y[n & 7] + n;
     }
-    if constexpr (GX) {
+    if constexpr (GX == 1) {
       const uint64_t P0 = (static_cast<uint64_t>(o[0][1]) << 32) | o[0][0];   // rows 0-3
       const uint64_t P1 = (static_cast<uint64_t>(o[0][3]) << 32) | o[0][2];   // rows 4-7
       asm volatile(NTC_GX_CHAIN : NTC_GX_OUTS(A) : NTC_GX_INS(Y, P0, P1) : NTC_GX_CLOBBERS);
+      continue;
+    } else if constexpr (GX == 2) {
+      const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
+      asm volatile(NTC_GX2_CHAIN : NTC_GX_OUTS(A) : NTC_GX2_INS(Y, P) : NTC_GX2_CLOBBERS);
       continue;
     } else {
     uint32_t O[16 * NJ];
@@ -655,7 +666,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #endif
 constexpr int kBjWaves = NTC_BJ_WPB;     // waves (independent tasks) per workgroup; tuning builds
 
-template <int RT, bool DEC, int ABL = 0, bool GX = false>
+template <int RT, bool DEC, int ABL = 0, int GX = 0>
 #ifndef NTC_BJ_WAVES_PER_EU
 #define NTC_BJ_WAVES_PER_EU 1
 #endif
@@ -685,8 +696,8 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_
       return;
     }
   }
-  if constexpr (GX) {
-    mac_tile_bj<8, RT, DEC, ABL, true>(a, g, tile, nrows, cc, lane, ring_p, ring);
+  if constexpr (GX != 0) {
+    mac_tile_bj<8, RT, DEC, ABL, GX>(a, g, tile, nrows, cc, lane, ring_p, ring);
     return;
   }
   if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
@@ -1902,12 +1913,14 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
   return pieces * 100 >= spans * 128 * 70;
 }
 
-// NTC_GF256_BJ_GX=1: the bit-sliced MAC runs the shared-table chain (gf_bitslice_gidx.inc).
-bool gx_chain()
+// NTC_GF256_BJ_GX=1|2: the bit-sliced MAC runs a shared-table chain (gf_bitslice_gidx.inc):
+// 1 = packed u16 block offsets (gx_offsets kernel), 2 = coefficient bytes, fixed 128-B blocks.
+int gx_chain()
 {
-  static const bool gx = [] {
+  static const int gx = [] {
     const char* v = std::getenv("NTC_GF256_BJ_GX");
-    return v && std::atoi(v) == 1;
+    const int x = v ? std::atoi(v) : 0;
+    return x == 1 || x == 2 ? x : 0;
   }();
   return gx;
 }
@@ -1921,11 +1934,14 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   uint32_t rowtile = 32, span;
   uint64_t blk_align = 1;
   if (use_bitslice(e, a.stride) && gx_chain()) {
-    // shared-table chain: block offsets from the coefficient bytes (gx_offsets), 8-row tiles
+    // shared-table chain, 8-row tiles: block offsets from the coefficient bytes (gx_offsets,
+    // variant 1) or the coefficient bytes themselves (variant 2)
     rowtile = 8;
     span = 2048;
     blk_align = 8;
-    fn = dec ? gf_mac_bj<8, true, 0, true> : gf_mac_bj<8, false, 0, true>;
+    const int gv = gx_chain();
+    fn = gv == 2 ? (dec ? gf_mac_bj<8, true, 0, 2> : gf_mac_bj<8, false, 0, 2>)
+                 : (dec ? gf_mac_bj<8, true, 0, 1> : gf_mac_bj<8, false, 0, 1>);
     a.ntiles = (a.rows + 7) / 8;
     if (dec) {
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
@@ -1940,16 +1956,18 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
       a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
     }
-    const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles;
-    int rc = ensure_buf(&e->joff, &e->joff_cap, n * 16, "hipMalloc gx offsets");
-    if (rc) return rc;
-    a.joff = static_cast<const uint32_t*>(e->joff);
-    {
-      KernelTimer kt(e, NTC_GF256_K_BJ_OFFSETS, st);
-      hipLaunchKernelGGL(gx_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
-                         a.coef, a.rp, a.ntiles, n, static_cast<uint32_t*>(e->joff));
+    if (gv == 1) {
+      const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles;
+      int rc = ensure_buf(&e->joff, &e->joff_cap, n * 16, "hipMalloc gx offsets");
+      if (rc) return rc;
+      a.joff = static_cast<const uint32_t*>(e->joff);
+      {
+        KernelTimer kt(e, NTC_GF256_K_BJ_OFFSETS, st);
+        hipLaunchKernelGGL(gx_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
+                           a.coef, a.rp, a.ntiles, n, static_cast<uint32_t*>(e->joff));
+      }
+      if ((rc = hip_check(hipGetLastError(), "gx_offsets launch"))) return rc;
     }
-    if ((rc = hip_check(hipGetLastError(), "gx_offsets launch"))) return rc;
   } else if (use_bitslice(e, a.stride)) {
     static const uint32_t rt = [] {
       const char* v = std::getenv("NTC_GF256_BJ_ROWS");      // 8 | 16 (tuning experiments)

@@ -139,6 +139,62 @@ def chain(off, span):
     return lines
 
 
+# ---- variant 2: raw coefficient bytes, fixed 128-byte blocks, one 64-bit row register -------
+# P holds the 8 rows' coefficients (row 0 in the low byte).  Block c sits at c * 128; its tail
+# shifts P right by a byte (SCC = rows left, else leave), turns the new low byte into its block
+# address with two shifts (no literal), advances the VGPR index by adding 8 to M0 directly
+# (M0[7:0] is the index s_set_gpr_idx_on set; the mode bits sit in M0[15:12]) and jumps.
+BLK2 = 128
+
+
+def tail2(safe):
+    t = ["s_lshr_b64 s[90:91], s[90:91], 8",           # next row's coefficient; SCC = rows left
+         "s_cbranch_scc0 LQe%=",
+         "s_lshl_b32 s98, s90, 24",
+         "s_lshr_b32 s98, s98, 17",                      # c << 7
+         "s_add_u32 s98, s96, s98"]
+    if safe:
+        t.append("s_addc_u32 s99, s97, 0")
+    t += ["s_add_u32 m0, m0, 8",                        # next row: VGPR index + 8
+          "s_setpc_b64 s[98:99]"]
+    return t
+
+
+def copy2(safe):
+    tag = "s" if safe else "f"
+    lo, hi, _ = table_planes()
+    lines = [".p2align 7", f"LQu{tag}%=:"]
+    for c in range(256):
+        lab = f"LQv{tag}{c}_%="
+        lines.append(f"{lab}:")
+        lines += byte_ops(lo, hi, c) + tail2(safe)
+        lines.append(f".fill {BLK2} - (. - {lab}), 1, 0")
+    return lines
+
+
+def chain2():
+    span = 256 * BLK2
+    first = ["s_mov_b64 s[90:91], %[p]",
+             "s_cmp_eq_u64 s[90:91], 0", "s_cbranch_scc1 LQe%=",
+             "s_lshl_b32 s98, s90, 24", "s_lshr_b32 s98, s98, 17",
+             "s_add_u32 s98, s96, s98"]
+    lines = ["s_mov_b32 s94, m0",
+             "s_getpc_b64 s[96:97]", "LQg%=:",
+             "s_add_u32 s96, s96, LQuf%= - LQg%=", "s_addc_u32 s97, s97, 0",
+             f"s_add_u32 s98, s96, {span}", "s_cbranch_scc1 LQsafe%=",
+             "s_mov_b32 s99, s97",
+             "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)"]
+    lines += first + ["s_setpc_b64 s[98:99]"]
+    lines += copy2(False)
+    lines += ["LQsafe%=:", "s_getpc_b64 s[96:97]", "LQh%=:",
+              "s_add_u32 s96, s96, LQus%= - LQh%=", "s_addc_u32 s97, s97, 0",
+              "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)"]
+    lines += first + ["s_addc_u32 s99, s97, 0", "s_setpc_b64 s[98:99]"]
+    lines += copy2(True)
+    lines += ["LQe%=:", "s_set_gpr_idx_off", "s_mov_b32 m0, s94"]
+    return lines
+
+
 def main():
     off, span = layout()
     assert span < 65536, span
@@ -159,6 +215,13 @@ def main():
     ins += ', [p0] "s"(P0), [p1] "s"(P1)'
     o.append(f"#define NTC_GX_INS(Y, P0, P1) {ins}")
     o.append('#define NTC_GX_CLOBBERS "s90", "s91", "s94", "s95", "s96", "s97", "s98", "s99", "scc"')
+    o.append("")
+    o.append("// variant 2: P = the 8 rows' coefficient bytes (row 0 lowest); fixed 128-byte blocks")
+    o.append("#define NTC_GX2_CHAIN \\")
+    o.append("".join(f'  "{l}\\n" \\\n' for l in chain2()) + '  ""')
+    o.append('#define NTC_GX2_INS(Y, P) ' + ", ".join(f'[y{n}] "v"(Y[{n}])' for n in range(NPLANES)) +
+             ', [p] "s"(P)')
+    o.append('#define NTC_GX2_CLOBBERS "s90", "s91", "s94", "s96", "s97", "s98", "s99", "scc"')
     open(OUT, "w").write("\n".join(o) + "\n")
     print("wrote", OUT, "table bytes", span)
 

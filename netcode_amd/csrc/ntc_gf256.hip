@@ -362,6 +362,10 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
 // tools/gen_bitslice_gidx.py.
 #include "gf_bitslice_gidx.inc"
 
+// Variant 3's block table, once per code object: never called (it starts with s_endpgm); the MAC
+// kernels enter it with s_swappc and it returns through s92:93.
+extern "C" __device__ __attribute__((used, noinline)) void ntc_gx3_tables() { asm volatile(NTC_GX3_TABLES); }
+
 // Delta swap of the `mask` bit groups of b with the groups `sh` bits higher in a: two shifts and
 // two bit-field inserts (v_bfi_b32 / v_bitop3), 4 VALU.
 __device__ __forceinline__ void swap_blocks(uint32_t& a, uint32_t& b, uint32_t sh, uint32_t mask)
@@ -503,13 +507,13 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
   constexpr uint32_t kOffDw = GX == 1 ? 4u : 2u * RT;   // offset dwords per (source, tile)
   // GX = 2: one source's coefficient row is rp bytes (rp % 4 == 0); the tile's 8 start at 8*tile
-  const uint32_t jstep = GX == 2 ? a.rp / 4u : a.ntiles * kOffDw;
-  const uint32_t* jrow = GX == 2
+  const uint32_t jstep = GX >= 2 ? a.rp / 4u : a.ntiles * kOffDw;
+  const uint32_t* jrow = GX >= 2
       ? reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * 8u)
       : a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * kOffDw;
   constexpr int NJ = R == 16 ? 2 : 1;     // offset vectors per source
   using OffV = typename std::conditional<GX == 1, u32x4,
-               typename std::conditional<GX == 2, u32x2, u32x16>::type>::type;
+               typename std::conditional<GX >= 2, u32x2, u32x16>::type>::type;
   const uint64_t pmask = a.rp >= 8 ? ~0ull : 0xFFFFFFFFull;   // rp = 4: bytes 4-7 = next source
   // Offsets and row addresses are loaded with ordinary uniform loads through the constant address
   // space (s_load, waits placed by the compiler).  Decode reads each input row's address from the
@@ -533,6 +537,22 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
   for (int j = 0; j < (GX ? R : 1); ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
   (void)pmask;
+  uint64_t tbase = 0;           // GX = 3: the block table (fast copy, or the safe one if the fast
+  if constexpr (GX == 3) {      // copy straddles a 4 GiB boundary), located once per wave
+    asm volatile("s_getpc_b64 s[96:97]\n"
+                 "LT3a%=:\n"
+                 "s_add_u32 s96, s96, ntc_gx3_f - LT3a%=\n"
+                 "s_addc_u32 s97, s97, 0\n"
+                 "s_add_u32 s98, s96, 32768\n"
+                 "s_cbranch_scc0 LT3o%=\n"
+                 "s_getpc_b64 s[96:97]\n"
+                 "LT3b%=:\n"
+                 "s_add_u32 s96, s96, ntc_gx3_s - LT3b%=\n"
+                 "s_addc_u32 s97, s97, 0\n"
+                 "LT3o%=:\n"
+                 "s_mov_b64 %0, s[96:97]\n"
+                 : "=s"(tbase) :: "s96", "s97", "s98", "scc");
+  }
 
   // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait counts are constant);
   // source 0 read into registers.  Steady state at iteration i: source i in registers, the LDS
@@ -603,6 +623,26 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     } else if constexpr (GX == 2) {
       const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
       asm volatile(NTC_GX2_CHAIN : NTC_GX_OUTS(A) : NTC_GX2_INS(Y, P) : NTC_GX2_CLOBBERS);
+      continue;
+    } else if constexpr (GX == 3) {
+      const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
+      asm volatile("s_mov_b32 s94, m0\n"
+                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                   "s_mov_b64 s[96:97], %[tb]\n"
+                   "s_mov_b64 s[90:91], %[p]\n"
+                   "s_cmp_eq_u64 s[90:91], 0\n"
+                   "s_cbranch_scc1 LT3d%=\n"
+                   "s_lshl_b32 s98, s90, 24\n"
+                   "s_lshr_b32 s98, s98, 17\n"
+                   "s_add_u32 s98, s96, s98\n"
+                   "s_addc_u32 s99, s97, 0\n"
+                   "s_swappc_b64 s[92:93], s[98:99]\n"
+                   "LT3d%=:\n"
+                   "s_set_gpr_idx_off\n"
+                   "s_mov_b32 m0, s94\n"
+                   : NTC_GX_OUTS(A)
+                   : NTC_GX3_YPINS(Y), [p] "s"(P), [tb] "s"(tbase)
+                   : "s90", "s91", "s92", "s93", "s94", "s96", "s97", "s98", "s99", "scc");
       continue;
     } else {
     uint32_t O[16 * NJ];
@@ -1920,7 +1960,7 @@ int gx_chain()
   static const int gx = [] {
     const char* v = std::getenv("NTC_GF256_BJ_GX");
     const int x = v ? std::atoi(v) : 0;
-    return x == 1 || x == 2 ? x : 0;
+    return x >= 1 && x <= 3 ? x : 0;
   }();
   return gx;
 }
@@ -1940,7 +1980,8 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     span = 2048;
     blk_align = 8;
     const int gv = gx_chain();
-    fn = gv == 2 ? (dec ? gf_mac_bj<8, true, 0, 2> : gf_mac_bj<8, false, 0, 2>)
+    fn = gv == 3 ? (dec ? gf_mac_bj<8, true, 0, 3> : gf_mac_bj<8, false, 0, 3>)
+       : gv == 2 ? (dec ? gf_mac_bj<8, true, 0, 2> : gf_mac_bj<8, false, 0, 2>)
                  : (dec ? gf_mac_bj<8, true, 0, 1> : gf_mac_bj<8, false, 0, 1>);
     a.ntiles = (a.rows + 7) / 8;
     if (dec) {

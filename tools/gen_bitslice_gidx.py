@@ -195,6 +195,42 @@ def chain2():
     return lines
 
 
+# ---- variant 3: variant 2's table ONCE, outside the kernels --------------------------------
+# The 256 blocks live in a never-called holder function (ntc_gx3_tables), so the MAC loop body
+# stays small (short back edge) and every kernel shares one copy.  Fixed registers: table
+# planes Y[0..29] in v[Y3..Y3+29], accumulators v[ACC..ACC+63] (index-relative), s90:91 the row
+# coefficients, s96:97 the table base, s92:93 the return address (s_swappc at entry).  The fast
+# table keeps the jump target's high half fixed; the safe one (chosen once per kernel when the
+# fast table straddles a 4 GiB boundary) propagates the carry.
+Y3 = 32
+
+
+def byte_ops3(lo, hi, c):
+    return [op.replace("%[y", "%%[y") for op in byte_ops(lo, hi, c)]
+
+
+def table3(safe):
+    tag = "s" if safe else "f"
+    lo, hi, _ = table_planes()
+    ymap = {f"%[y{n}]": f"v{Y3 + n}" for n in range(NPLANES)}
+    lines = [".p2align 7", f"ntc_gx3_{tag}:"]
+    for c in range(256):
+        lab = f"ntc_gx3_{tag}{c}"
+        lines.append(f"{lab}:")
+        body = byte_ops(lo, hi, c)
+        for k, v in sorted(ymap.items(), key=lambda kv: -len(kv[0])):
+            body = [b.replace(k, v) for b in body]
+        t = ["s_lshr_b64 s[90:91], s[90:91], 8", f"s_cbranch_scc0 ntc_gx3_ret_{tag}",
+             "s_lshl_b32 s98, s90, 24", "s_lshr_b32 s98, s98, 17", "s_add_u32 s98, s96, s98"]
+        if safe:
+            t.append("s_addc_u32 s99, s97, 0")
+        t += ["s_add_u32 m0, m0, 8", "s_setpc_b64 s[98:99]"]
+        lines += body + t
+        lines.append(f".fill {BLK2} - (. - {lab}), 1, 0")
+    lines += [f"ntc_gx3_ret_{tag}:", "s_setpc_b64 s[92:93]"]
+    return lines
+
+
 def main():
     off, span = layout()
     assert span < 65536, span
@@ -222,6 +258,13 @@ def main():
     o.append('#define NTC_GX2_INS(Y, P) ' + ", ".join(f'[y{n}] "v"(Y[{n}])' for n in range(NPLANES)) +
              ', [p] "s"(P)')
     o.append('#define NTC_GX2_CLOBBERS "s90", "s91", "s94", "s96", "s97", "s98", "s99", "scc"')
+    o.append("")
+    o.append("// variant 3: the tables (fast, then safe) for the holder function ntc_gx3_tables")
+    o.append(f"constexpr int kGx3Y = {Y3};                  // first table-plane VGPR (Y[0])")
+    o.append(f"constexpr uint32_t kGx3Span = {256 * BLK2};")
+    o.append("#define NTC_GX3_TABLES \\")
+    o.append("".join(f'  "{l}\\n" \\\n' for l in ["s_endpgm"] + table3(False) + table3(True)) + '  ""')
+    o.append('#define NTC_GX3_YPINS(Y) ' + ", ".join(f'[y{n}] "{{v{Y3 + n}}}"(Y[{n}])' for n in range(NPLANES)))
     open(OUT, "w").write("\n".join(o) + "\n")
     print("wrote", OUT, "table bytes", span)
 

@@ -10,7 +10,7 @@ typedef struct ntc_data_t ntc_data_t;
 
 ntc_data_t* ntc_new_data(uint16_t size) NTC_C_NOEXCEPT;                  /* NULL on OOM */
 ntc_data_t* ntc_new_data_from(const char* src, uint16_t size) NTC_C_NOEXCEPT NTC_C_NONNULL;
-void        ntc_delete_data(ntc_data_t* data) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void        ntc_delete_data(ntc_data_t* data) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 char*       ntc_data_buffer(ntc_data_t* data) NTC_C_NOEXCEPT NTC_C_NONNULL;   /* 16-B aligned */
 uint16_t    ntc_data_get_size(const ntc_data_t* data) NTC_C_NOEXCEPT NTC_C_NONNULL;
 void        ntc_data_resize(ntc_data_t* data, uint16_t new_size, ntc_error* error)

@@ -14,7 +14,7 @@ typedef enum { ntc_in_order_yes, ntc_in_order_no } ntc_ordering_type;
 ntc_decoder_t* ntc_new_decoder(uint8_t galois_field_size, ntc_ordering_type order,
                                ntc_packet_handler packet_handler, ntc_data_handler data_handler)
                NTC_C_NOEXCEPT;
-void   ntc_delete_decoder(ntc_decoder_t* dec) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void   ntc_delete_decoder(ntc_decoder_t* dec) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 /* Consumes `packet` (a source or a repair); returns the number of bytes read. */
 size_t ntc_decoder_add_packet(ntc_decoder_t* dec, ntc_packet_t* packet, ntc_error* error)
        NTC_C_NOEXCEPT NTC_C_NONNULL;

@@ -14,7 +14,7 @@ typedef enum { ntc_systematic_yes, ntc_systematic_no } ntc_code_type;
 
 /* galois_field_size: 4, 8, 16 or 32; NULL on OOM, unsupported size or no MI355X engine. */
 ntc_encoder_t* ntc_new_encoder(uint8_t galois_field_size, ntc_packet_handler handler) NTC_C_NOEXCEPT;
-void   ntc_delete_encoder(ntc_encoder_t* enc) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void   ntc_delete_encoder(ntc_encoder_t* enc) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 /* Consumes `data` (left empty: resize or delete it afterwards). */
 void   ntc_encoder_add_data(ntc_encoder_t* enc, ntc_data_t* data, ntc_error* error)
        NTC_C_NOEXCEPT NTC_C_NONNULL;

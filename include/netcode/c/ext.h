@@ -36,11 +36,31 @@ size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT N
  * event and detaches its objects. */
 typedef struct ntc_batch_t ntc_batch_t;
 ntc_batch_t* ntc_new_batch(void) NTC_C_NOEXCEPT;
-void ntc_delete_batch(ntc_batch_t* batch) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void ntc_delete_batch(ntc_batch_t* batch) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 void ntc_encoder_set_batch(ntc_encoder_t* enc, ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT;
 void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT;
 void ntc_batch_flush(ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT NTC_C_NONNULL;
 size_t ntc_batch_pending(const ntc_batch_t* batch) NTC_C_NOEXCEPT NTC_C_NONNULL;
+
+/* GF(2^w) region work on host buffers, run on the MI355X engine (one H2D, one combine launch,
+ * one D2H): the region operations of the C++ detail layer (include/netcode/detail/galois_field.hh,
+ * encoder.hh, decoder.hh -- the reference's galois_field::multiply / multiply_add call sites,
+ * galois_field.hh:65-92, detail/encoder.cc:35-57, detail/decoder.cc:173, 407, 524-532).
+ *   ntc_gf_combine_host:      out[0..out_len) = sum_i coefs[i] * in_i, each input read over
+ *                             lens[i] bytes and zero-extended; add = 1 XORs the sum into out.
+ *   ntc_gf_combine_rows_host: rows outputs from the same inputs, out_s = sum_i coefs[i * rows + s]
+ *                             * in_i (full decoding's M^-1 application).
+ * w in {4, 8, 16, 32}; lengths <= 65535.  Return 0, or -1 with error set (no device, bad w). */
+int ntc_gf_combine_host(uint32_t w, size_t n, const char* const* in, const uint16_t* lens,
+                        const uint32_t* coefs, size_t out_len, char* out, int add,
+                        ntc_error* error) NTC_C_NOEXCEPT;
+int ntc_gf_combine_rows_host(uint32_t w, size_t n, const char* const* in, const uint16_t* lens,
+                             size_t rows, const uint32_t* coefs, size_t out_len, char* const* out,
+                             ntc_error* error) NTC_C_NOEXCEPT;
+
+/* ntc::decoder::maybe_ack (reference decoder.hh:231-248): send an ack if the received-packet
+ * threshold or the ack period has been reached. */
+void ntc_decoder_maybe_ack(ntc_decoder_t* dec, ntc_error* error) NTC_C_NOEXCEPT NTC_C_NONNULL;
 
 #ifdef __cplusplus
 }

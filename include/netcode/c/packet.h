@@ -12,7 +12,7 @@ typedef struct ntc_packet_t ntc_packet_t;
 
 ntc_packet_t* ntc_new_packet(uint16_t size) NTC_C_NOEXCEPT;              /* NULL on OOM */
 ntc_packet_t* ntc_new_packet_from(const char* src, uint16_t size) NTC_C_NOEXCEPT NTC_C_NONNULL;
-void          ntc_delete_packet(ntc_packet_t* packet) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void          ntc_delete_packet(ntc_packet_t* packet) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 char*         ntc_packet_buffer(ntc_packet_t* packet) NTC_C_NOEXCEPT NTC_C_NONNULL;
 uint16_t      ntc_packet_get_size(const ntc_packet_t* packet) NTC_C_NOEXCEPT NTC_C_NONNULL;
 void          ntc_packet_resize(ntc_packet_t* packet, uint16_t new_size, ntc_error* error)

@@ -12,6 +12,7 @@
 #include <utility>
 
 #include "netcode/detail/c_bridge.hh"
+#include "netcode/detail/packetizer.hh"   // the reference's public headers expose the wire layer
 #include "netcode/errors.hh"
 #include "netcode/in_order.hh"
 #include "netcode/packet.hh"
@@ -85,6 +86,16 @@ public:
   {
     ntc_error e{ntc_no_error, nullptr};
     ntc_decoder_generate_ack(m_dec, &e);
+    m_pending.rethrow();
+    detail::throw_on(e);
+  }
+
+  /// Send an ack if enough packets arrived or the ack period elapsed (reference decoder.hh:
+  /// 231-248; also run after every delivery).
+  void maybe_ack()
+  {
+    ntc_error e{ntc_no_error, nullptr};
+    ntc_decoder_maybe_ack(m_dec, &e);
     m_pending.rethrow();
     detail::throw_on(e);
   }

@@ -11,6 +11,7 @@
 
 #include "netcode/data.hh"
 #include "netcode/detail/c_bridge.hh"
+#include "netcode/detail/packetizer.hh"   // the reference's public headers expose the wire layer
 #include "netcode/errors.hh"
 #include "netcode/packet.hh"
 #include "netcode/systematic.hh"

@@ -73,7 +73,12 @@ CPP_CHECKS = {
     # the reference's Catch unit tests (ctest UnitTests, tests/CMakeLists.txt:1-29) that compile
     # against this repo's headers; linked with the reference's Catch main (tests/tests.cc)
     "ref_unit_public": ([REF + "/tests/netcode/test_packet.cc", REF + "/tests/netcode/c/test_data.cc",
-                         REF + "/tests/netcode/c/test_decoder.cc"], True),
+                         REF + "/tests/netcode/c/test_decoder.cc", REF + "/tests/netcode/test_encoder.cc",
+                         REF + "/tests/netcode/test_decoder.cc"], True),
+    # the detail layer (include/netcode/detail/*.hh)
+    "ref_unit_detail": ([REF + "/tests/netcode/detail/" + f for f in (
+        "test_buffer.cc", "test_galois_field.cc", "test_square_matrix.cc", "test_source_list.cc",
+        "test_encoder.cc", "test_decoder.cc")] + [REF + "/tests/netcode/test_reconstruction.cc"], True),
 }
 
 

@@ -669,6 +669,13 @@ class Decoder {
     } else {
       dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.sym.data()), s.size);
     }
+    maybe_ack();
+  }
+
+ public:
+  // decoder.hh:231-248: ack once enough packets arrived or the ack period elapsed
+  void maybe_ack()
+  {
     if (ack_packets_ >= ack_nb_packets_) {
       generate_ack();
       last_ack_ = std::chrono::steady_clock::now();
@@ -680,6 +687,8 @@ class Decoder {
       }
     }
   }
+
+ private:
   void deliver_id(uint32_t id)
   {
     auto it = sources_.find(id);
@@ -1315,5 +1324,58 @@ void ntc_batch_flush(ntc_batch_t* b, ntc_error* error) noexcept
   ntcx::guarded([&] { b->b.flush(); }, error);
 }
 size_t ntc_batch_pending(const ntc_batch_t* b) noexcept { return b->b.pending(); }
+
+void ntc_decoder_maybe_ack(ntc_decoder_t* dec, ntc_error* error) noexcept
+{
+  ntcx::guarded([&] { dec->d.maybe_ack(); }, error);
+}
+
+int ntc_gf_combine_host(uint32_t w, size_t n, const char* const* in, const uint16_t* lens,
+                        const uint32_t* coefs, size_t out_len, char* out, int add,
+                        ntc_error* error) noexcept
+{
+  ntc_error local{ntc_no_error, nullptr};
+  ntc_error* err = error ? error : &local;
+  return ntcx::guarded([&]() -> int {
+    const ntcx::Field f(w);                       // rejects w outside {4, 8, 16, 32}
+    (void)f;
+    if (out_len > 0xFFFF) throw std::invalid_argument("region longer than 65535 bytes");
+    std::vector<const uint8_t*> ins;
+    std::vector<uint16_t> ls;
+    std::vector<uint32_t> cs;
+    if (add) {                                    // out ^= sum: out itself is a term (staged first)
+      ins.push_back(reinterpret_cast<const uint8_t*>(out));
+      ls.push_back(static_cast<uint16_t>(out_len));
+      cs.push_back(1);
+    }
+    for (size_t i = 0; i < n; ++i) {
+      ins.push_back(reinterpret_cast<const uint8_t*>(in[i]));
+      ls.push_back(static_cast<uint16_t>(std::min<size_t>(lens[i], out_len)));
+      cs.push_back(coefs[i]);
+    }
+    if (out_len) ntcx::Device::get().combine(w, ins.size(), ins.data(), ls.data(), cs.data(), out_len,
+                                            reinterpret_cast<uint8_t*>(out));
+    return 0;
+  }, err) == 0 && err->type == ntc_no_error ? 0 : -1;
+}
+
+int ntc_gf_combine_rows_host(uint32_t w, size_t n, const char* const* in, const uint16_t* lens,
+                             size_t rows, const uint32_t* coefs, size_t out_len, char* const* out,
+                             ntc_error* error) noexcept
+{
+  ntc_error local{ntc_no_error, nullptr};
+  ntc_error* err = error ? error : &local;
+  return ntcx::guarded([&]() -> int {
+    const ntcx::Field f(w);
+    (void)f;
+    if (out_len > 0xFFFF) throw std::invalid_argument("region longer than 65535 bytes");
+    if (rows == 0 || out_len == 0) return 0;
+    std::vector<uint8_t*> outs(rows);
+    for (size_t s = 0; s < rows; ++s) outs[s] = reinterpret_cast<uint8_t*>(out[s]);
+    ntcx::Device::get().combine_rows(w, n, reinterpret_cast<const uint8_t* const*>(in), lens, rows,
+                                     coefs, out_len, outs.data());
+    return 0;
+  }, err) == 0 && err->type == ntc_no_error ? 0 : -1;
+}
 
 }  // extern "C"

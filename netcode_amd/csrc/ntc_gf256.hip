@@ -539,16 +539,18 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   (void)pmask;
   uint64_t tbase = 0;           // GX = 3: the block table (fast copy, or the safe one if the fast
   if constexpr (GX == 3) {      // copy straddles a 4 GiB boundary), located once per wave
+    // the table sits anywhere in the code object (before this kernel, typically): the PC-relative
+    // offset is a signed 64-bit quantity, added as low half + high half with carry
+    // (the standard PC-relative pair: s_getpc returns the s_add's address; the lo literal sits
+    // 4 bytes after it, the hi literal 12)
     asm volatile("s_getpc_b64 s[96:97]\n"
-                 "LT3a%=:\n"
-                 "s_add_u32 s96, s96, ntc_gx3_f - LT3a%=\n"
-                 "s_addc_u32 s97, s97, 0\n"
+                 "s_add_u32 s96, s96, ntc_gx3_f@rel32@lo+4\n"
+                 "s_addc_u32 s97, s97, ntc_gx3_f@rel32@hi+12\n"
                  "s_add_u32 s98, s96, 32768\n"
                  "s_cbranch_scc0 LT3o%=\n"
                  "s_getpc_b64 s[96:97]\n"
-                 "LT3b%=:\n"
-                 "s_add_u32 s96, s96, ntc_gx3_s - LT3b%=\n"
-                 "s_addc_u32 s97, s97, 0\n"
+                 "s_add_u32 s96, s96, ntc_gx3_s@rel32@lo+4\n"
+                 "s_addc_u32 s97, s97, ntc_gx3_s@rel32@hi+12\n"
                  "LT3o%=:\n"
                  "s_mov_b64 %0, s[96:97]\n"
                  : "=s"(tbase) :: "s96", "s97", "s98", "scc");

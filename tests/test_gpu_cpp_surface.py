@@ -86,3 +86,16 @@ def test_reference_unit_tests_public(gpu):
     r = _run("ref_unit_public", timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "All tests passed" in r.stdout, r.stdout
+
+
+def test_reference_unit_tests_detail(gpu):
+    """The reference's Catch tests of its detail layer against include/netcode/detail/*.hh (region
+    work on the MI355X engine): test_buffer, test_galois_field (x * 1/x = 1 for w = 4/8/16/32),
+    test_square_matrix, test_source_list, detail/test_encoder, detail/test_decoder (reconstruct,
+    remove, useless, missing, outdated, 2- and 5-loss full decodings, duplicates, ordering) and
+    test_reconstruction.  Not compiled (they need Boost, absent from the image):
+    test_invert_matrix.cc (boost/optional/optional_io.hpp) and test_packetizer.cc
+    (boost::endian); test_serialize_packet.cc covers the out-of-scope packet dump aid."""
+    r = _run("ref_unit_detail", timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "All tests passed" in r.stdout, r.stdout[-2000:]

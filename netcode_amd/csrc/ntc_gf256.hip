@@ -1955,14 +1955,18 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
   return pieces * 100 >= spans * 128 * 70;
 }
 
-// NTC_GF256_BJ_GX=1|2: the bit-sliced MAC runs a shared-table chain (gf_bitslice_gidx.inc):
-// 1 = packed u16 block offsets (gx_offsets kernel), 2 = coefficient bytes, fixed 128-B blocks.
+// The bit-sliced MAC's chain (gf_bitslice_gidx.inc / gf_bitslice_chain.inc).  Default 3: one
+// shared 256-block table outside the kernels, one dispatch per (source, row), coefficient bytes
+// read directly.  NTC_GF256_BJ_GX=0|1|2 selects the earlier forms for A/B runs: 0 = per-site
+// nibble tables (two dispatches per row), 1 = in-kernel table with packed u16 offsets
+// (gx_offsets kernel), 2 = in-kernel table, coefficient bytes.
 int gx_chain()
 {
   static const int gx = [] {
     const char* v = std::getenv("NTC_GF256_BJ_GX");
-    const int x = v ? std::atoi(v) : 0;
-    return x >= 1 && x <= 3 ? x : 0;
+    if (!v) return 3;
+    const int x = std::atoi(v);
+    return x >= 0 && x <= 3 ? x : 3;
   }();
   return gx;
 }
@@ -2155,9 +2159,9 @@ const char* ntc_gf256_last_error(void) { return g_err.c_str(); }
 
 const char* ntc_gf256_build_info(void)
 {
-  return "libntc_gf256 gfx950: bit-sliced jump-chained XOR MAC (32 B lanes, 8-row tiles) for strides "
-         "filling >= 70 % of a 2 KiB wave span; v_perm_b32 3/3/2 split MAC (R in {4,8,16,32}, D in "
-         "{1,2,4}) otherwise";
+  return "libntc_gf256 gfx950: bit-sliced XOR MAC (32 B lanes, 8-row tiles, one shared 256-block "
+         "table entered per row with VGPR-relative accumulators) for strides filling >= 70 % of a "
+         "2 KiB wave span; v_perm_b32 3/3/2 split MAC (R in {4,8,16,32}, D in {1,2,4}) otherwise";
 }
 
 uint32_t ntc_gf256_coefficient(uint32_t repair_id, uint32_t src_id) { return coefficient(repair_id, src_id); }

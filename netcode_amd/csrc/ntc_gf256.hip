@@ -497,7 +497,7 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
                                             const uint8_t* ring_p, uint32_t ring)
 {
-  static_assert(!GX || R == 8 || (GX == 4 && R == 16), "shared-table chains: 8-row tiles (16 for GX 4)");
+  static_assert(!GX || R == 8, "the shared-table chain works on 8-row tiles");
   const size_t stride = a.stride;
   const uint32_t k = a.k;
   const uint32_t c0 = cc * 2048u + lane * 16u, c1 = c0 + 1024u;
@@ -509,12 +509,11 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   // GX = 2: one source's coefficient row is rp bytes (rp % 4 == 0); the tile's 8 start at 8*tile
   const uint32_t jstep = GX >= 2 ? a.rp / 4u : a.ntiles * kOffDw;
   const uint32_t* jrow = GX >= 2
-      ? reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * (GX == 4 ? 16u : 8u))
+      ? reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * 8u)
       : a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * kOffDw;
   constexpr int NJ = R == 16 ? 2 : 1;     // offset vectors per source
   using OffV = typename std::conditional<GX == 1, u32x4,
-               typename std::conditional<GX == 4, u32x4,
-               typename std::conditional<GX >= 2, u32x2, u32x16>::type>::type>::type;
+               typename std::conditional<GX >= 2, u32x2, u32x16>::type>::type;
   const uint64_t pmask = a.rp >= 8 ? ~0ull : 0xFFFFFFFFull;   // rp = 4: bytes 4-7 = next source
   // Offsets and row addresses are loaded with ordinary uniform loads through the constant address
   // space (s_load, waits placed by the compiler).  Decode reads each input row's address from the
@@ -538,8 +537,8 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
 #pragma unroll
   for (int j = 0; j < (GX ? R : 1); ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
   (void)pmask;
-  uint64_t tbase = 0;           // GX >= 3: the block table (fast copy, or the safe one if the
-  if constexpr (GX >= 3) {      // fast copy straddles a 4 GiB boundary), located once per wave
+  uint64_t tbase = 0;           // GX = 3: the block table (fast copy, or the safe one if the fast
+  if constexpr (GX == 3) {      // copy straddles a 4 GiB boundary), located once per wave
     // the table sits anywhere in the code object (before this kernel, typically): the PC-relative
     // offset is a signed 64-bit quantity, added as low half + high half with carry
     // (the standard PC-relative pair: s_getpc returns the s_add's address; the lo literal sits
@@ -626,38 +625,6 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     } else if constexpr (GX == 2) {
       const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
       asm volatile(NTC_GX2_CHAIN : NTC_GX_OUTS(A) : NTC_GX2_INS(Y, P) : NTC_GX2_CLOBBERS);
-      continue;
-    } else if constexpr (GX == 4) {
-      // 16 rows: the table twice, rows 0-7 (index 0) then rows 8-15 (index 64)
-      const uint64_t P0 = (static_cast<uint64_t>(o[0][1]) << 32) | o[0][0];
-      const uint64_t P1 = (static_cast<uint64_t>(o[0][3]) << 32) | o[0][2];
-      asm volatile("s_mov_b32 s94, m0\n"
-                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-                   "s_mov_b64 s[96:97], %[tb]\n"
-                   "s_mov_b64 s[90:91], %[p0]\n"
-                   "s_cmp_eq_u64 s[90:91], 0\n"
-                   "s_cbranch_scc1 LT4h%=\n"
-                   "s_lshl_b32 s98, s90, 24\n"
-                   "s_lshr_b32 s98, s98, 17\n"
-                   "s_add_u32 s98, s96, s98\n"
-                   "s_addc_u32 s99, s97, 0\n"
-                   "s_swappc_b64 s[92:93], s[98:99]\n"
-                   "LT4h%=:\n"
-                   "s_set_gpr_idx_idx 64\n"
-                   "s_mov_b64 s[90:91], %[p1]\n"
-                   "s_cmp_eq_u64 s[90:91], 0\n"
-                   "s_cbranch_scc1 LT4d%=\n"
-                   "s_lshl_b32 s98, s90, 24\n"
-                   "s_lshr_b32 s98, s98, 17\n"
-                   "s_add_u32 s98, s96, s98\n"
-                   "s_addc_u32 s99, s97, 0\n"
-                   "s_swappc_b64 s[92:93], s[98:99]\n"
-                   "LT4d%=:\n"
-                   "s_set_gpr_idx_off\n"
-                   "s_mov_b32 m0, s94\n"
-                   : NTC_GX_OUTS16(A)
-                   : NTC_GX3_YPINS(Y), [p0] "s"(P0), [p1] "s"(P1), [tb] "s"(tbase)
-                   : "s90", "s91", "s92", "s93", "s94", "s96", "s97", "s98", "s99", "scc");
       continue;
     } else if constexpr (GX == 3) {
       const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
@@ -772,7 +739,7 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_
     }
   }
   if constexpr (GX != 0) {
-    mac_tile_bj<GX == 4 ? 16 : 8, RT, DEC, ABL, GX>(a, g, tile, nrows, cc, lane, ring_p, ring);
+    mac_tile_bj<8, RT, DEC, ABL, GX>(a, g, tile, nrows, cc, lane, ring_p, ring);
     return;
   }
   if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
@@ -1999,7 +1966,7 @@ int gx_chain()
     const char* v = std::getenv("NTC_GF256_BJ_GX");
     if (!v) return 3;
     const int x = std::atoi(v);
-    return x >= 0 && x <= 4 ? x : 3;
+    return x >= 0 && x <= 3 ? x : 3;
   }();
   return gx;
 }
@@ -2015,15 +1982,14 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   if (use_bitslice(e, a.stride) && gx_chain()) {
     // shared-table chain, 8-row tiles: block offsets from the coefficient bytes (gx_offsets,
     // variant 1) or the coefficient bytes themselves (variant 2)
-    const int gv = a.rp >= 16 ? gx_chain() : (gx_chain() == 4 ? 3 : gx_chain());   // 16-row tiles need rp >= 16
-    rowtile = gv == 4 ? 16 : 8;
+    rowtile = 8;
     span = 2048;
     blk_align = 8;
-    fn = gv == 4 ? (dec ? gf_mac_bj<16, true, 0, 4> : gf_mac_bj<16, false, 0, 4>)
-       : gv == 3 ? (dec ? gf_mac_bj<8, true, 0, 3> : gf_mac_bj<8, false, 0, 3>)
+    const int gv = gx_chain();
+    fn = gv == 3 ? (dec ? gf_mac_bj<8, true, 0, 3> : gf_mac_bj<8, false, 0, 3>)
        : gv == 2 ? (dec ? gf_mac_bj<8, true, 0, 2> : gf_mac_bj<8, false, 0, 2>)
                  : (dec ? gf_mac_bj<8, true, 0, 1> : gf_mac_bj<8, false, 0, 1>);
-    a.ntiles = (a.rows + rowtile - 1) / rowtile;
+    a.ntiles = (a.rows + 7) / 8;
     if (dec) {
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");

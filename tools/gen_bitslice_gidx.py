@@ -265,9 +265,6 @@ def main():
     o.append("#define NTC_GX3_TABLES \\")
     o.append("".join(f'  "{l}\\n" \\\n' for l in ["s_endpgm"] + table3(False) + table3(True)) + '  ""')
     o.append('#define NTC_GX3_YPINS(Y) ' + ", ".join(f'[y{n}] "{{v{Y3 + n}}}"(Y[{n}])' for n in range(NPLANES)))
-    o.append("// 16-row tiles (variant 4): accumulators of rows 0..15 at v[64 .. 191]")
-    outs16 = ", ".join(f'[A{j}] "+{{v[{ACC + 8 * j}:{ACC + 8 * j + 7}]}}"(A[{j}])' for j in range(16))
-    o.append(f"#define NTC_GX_OUTS16(A) {outs16}")
     open(OUT, "w").write("\n".join(o) + "\n")
     print("wrote", OUT, "table bytes", span)
 

@@ -212,6 +212,27 @@ int  ntc_gf256_read_packets(ntc_gf256_engine* eng, uint32_t npkts, const uint8_t
                             uint8_t* src, uint16_t* src_len, uint8_t* src_mask, uint8_t* rep,
                             uint16_t* rep_size, uint8_t* rep_mask, uint8_t* status, void* stream);
 
+/* ---- Packed rows <-> generation slots (host-resident batches) ---------------------------------
+ * A receiver holds only the sources it received and wants back only the ones it lost; these two
+ * byte movers let a host-resident caller ship exactly those over PCIe (the reference's decoder
+ * likewise stores received sources and hands out only recovered ones, decoder.hh: data_handler).
+ * Slot (g, i) is *selected* when (mask[g][i] != 0) == want; the selected slots of generation g
+ * map, in slot order, to packed rows row_base[g] - row0, row_base[g] - row0 + 1, ... of `packed`
+ * ([rows][stride]; row_base = the caller's prefix sum of selected counts, row0 lets a chunk of a
+ * batch use the batch's row_base with a chunk-relative packed buffer).
+ * ntc_gf256_unpack_slots  packed rows -> selected slots of slots [G][k][stride]; zero_rest != 0
+ *                         zeroes every slot that is not selected (e.g. the lost ones, so a
+ *                         generation that does not decode returns zeros).
+ * ntc_gf256_pack_slots    selected slots -> packed rows (e.g. want = 0: the recovered sources
+ *                         after ntc_gf256_decode_batch). */
+int  ntc_gf256_unpack_slots(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t stride,
+                            const uint8_t* packed, const uint32_t* row_base, uint32_t row0,
+                            const uint8_t* mask, uint8_t want, uint8_t* slots, int zero_rest,
+                            void* stream);
+int  ntc_gf256_pack_slots(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t stride,
+                          const uint8_t* slots, const uint8_t* mask, uint8_t want,
+                          const uint32_t* row_base, uint32_t row0, uint8_t* packed, void* stream);
+
 /* dst = c*src (add = 0) or dst ^= c*src (add = 1) over `len` bytes of device memory. */
 int  ntc_gf256_region_multiply(ntc_gf256_engine* eng, const uint8_t* src, uint8_t* dst,
                                size_t len, uint8_t c, int add, void* stream);

@@ -320,7 +320,70 @@ __global__ __launch_bounds__(kWireThreads) void wire_read_packets(ReadArgs a)
   if (threadIdx.x == 0) a.status[p] = static_cast<uint8_t>(st);
 }
 
+// ---- packed <-> slot layout (host-resident batches) -------------------------------------------
+
+struct PackArgs {
+  uint32_t G, k, stride, want, row0;
+  int zero_rest;                 // unpack: zero the slots not selected
+  const uint8_t* mask;
+  const uint32_t* row_base;
+  const uint8_t* from;
+  uint8_t* to;
+};
+
+// One workgroup per slot (g, i).  The slot is selected when (mask != 0) == want; its packed row
+// is row_base[g] - row0 + (selected slots of g before i), counted with one block-wide
+// __syncthreads_count per 256 slots.  UNPACK copies packed row -> slot, PACK slot -> packed row.
+template <bool UNPACK>
+__global__ __launch_bounds__(kWireThreads) void slot_pack(PackArgs a)
+{
+  const uint32_t p = blockIdx.x;
+  const uint32_t g = p / a.k, i = p % a.k;
+  const uint8_t* m = a.mask + static_cast<size_t>(g) * a.k;
+  const bool sel = (m[i] != 0) == (a.want != 0);          // uniform over the block
+  const uint32_t n16 = a.stride / 16u;
+  if (!sel) {
+    if (UNPACK && a.zero_rest) {
+      uint8_t* dst = a.to + static_cast<size_t>(p) * a.stride;
+      for (uint32_t c = threadIdx.x; c < n16; c += kWireThreads)
+        *reinterpret_cast<uint4*>(dst + 16u * c) = make_uint4(0, 0, 0, 0);
+    }
+    return;
+  }
+  uint32_t rank = 0;
+  for (uint32_t j0 = 0; j0 < i; j0 += kWireThreads) {
+    const uint32_t j = j0 + threadIdx.x;
+    rank += __syncthreads_count(j < i && (m[j] != 0) == (a.want != 0));
+  }
+  const size_t row = static_cast<size_t>(a.row_base[g] - a.row0 + rank);
+  const uint8_t* src = UNPACK ? a.from + row * a.stride : a.from + static_cast<size_t>(p) * a.stride;
+  uint8_t* dst = UNPACK ? a.to + static_cast<size_t>(p) * a.stride : a.to + row * a.stride;
+  for (uint32_t c = threadIdx.x; c < n16; c += kWireThreads)
+    *reinterpret_cast<uint4*>(dst + 16u * c) = *reinterpret_cast<const uint4*>(src + 16u * c);
+}
+
 uint32_t host_ids_bytes(uint32_t k) { return k == 0 ? 2u : 6u + 3u * ((k - 1u + 254u) / 255u); }
+
+int pack_launch(bool unpack, ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t stride,
+                const uint8_t* mask, uint32_t want, const uint32_t* row_base, uint32_t row0,
+                const uint8_t* from, uint8_t* to, int zero_rest, void* stream)
+{
+  if (!e || !mask || !row_base || !from || !to) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (G == 0 || k == 0) return fail(NTC_GPU_EINVAL, "G and k must be > 0");
+  if (stride == 0 || stride % 16 != 0 || stride > 65536)
+    return fail(NTC_GPU_EINVAL, "stride must be a non-zero multiple of 16, <= 65536");
+  const uint64_t n = static_cast<uint64_t>(G) * k;
+  if (n > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "too many slots for one launch");
+  (void)hipSetDevice(e->device);
+  PackArgs a{G, k, stride, want, row0, zero_rest, mask, row_base, from, to};
+  if (unpack)
+    hipLaunchKernelGGL(slot_pack<true>, dim3(static_cast<uint32_t>(n)), dim3(kWireThreads), 0,
+                       static_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(slot_pack<false>, dim3(static_cast<uint32_t>(n)), dim3(kWireThreads), 0,
+                       static_cast<hipStream_t>(stream), a);
+  return hip_check(hipGetLastError(), unpack ? "slot_unpack launch" : "slot_pack launch");
+}
 
 }  // namespace
 }  // namespace ntcgpu
@@ -398,6 +461,22 @@ int ntc_gf256_read_packets(ntc_gf256_engine* e, uint32_t npkts, const uint8_t* p
              src, src_len, src_mask, rep, rep_size, rep_mask, status};
   hipLaunchKernelGGL(wire_read_packets, dim3(npkts), dim3(kWireThreads), 0, st, a);
   return hip_check(hipGetLastError(), "wire_read_packets launch");
+}
+
+int ntc_gf256_unpack_slots(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t stride,
+                           const uint8_t* packed, const uint32_t* row_base, uint32_t row0,
+                           const uint8_t* mask, uint8_t want, uint8_t* slots, int zero_rest,
+                           void* stream)
+{
+  return pack_launch(true, e, G, k, stride, mask, want, row_base, row0, packed, slots, zero_rest,
+                     stream);
+}
+
+int ntc_gf256_pack_slots(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t stride,
+                         const uint8_t* slots, const uint8_t* mask, uint8_t want,
+                         const uint32_t* row_base, uint32_t row0, uint8_t* packed, void* stream)
+{
+  return pack_launch(false, e, G, k, stride, mask, want, row_base, row0, slots, packed, 0, stream);
 }
 
 }  // extern "C"

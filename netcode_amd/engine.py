@@ -328,7 +328,9 @@ class Wire:
       repair of an :class:`EncodeResult`;
     * :meth:`write_sources` -- ``packetizer::write_source`` (:165-183) for every source slot;
     * :meth:`read_packets` -- ``decoder::operator()(packet)`` dispatch + ``read_source`` /
-      ``read_repair`` (:125-158, 186-218) into the :class:`BatchDecoder` layout.
+      ``read_repair`` (:125-158, 186-218) into the :class:`BatchDecoder` layout;
+    * :meth:`unpack_slots` / :meth:`pack_slots` -- packed rows of only the received (or only the
+      lost) sources <-> the generation slots, so host-resident callers move just those bytes.
     """
 
     def __init__(self, device: int | torch.device = 0):
@@ -402,6 +404,40 @@ class Wire:
             out.rep_size.data_ptr(), out.rep_mask.data_ptr(), out.status.data_ptr(),
             _stream(dev)), "ntc_gf256_read_packets")
         return out
+
+    def _pack_args(self, slots, mask, row_base, packed, row0):
+        G, k, stride = slots.shape
+        dev = self.device
+        _require(slots, "slots", _U8, (G, k, stride), dev)
+        _require(mask, "mask", _U8, (G, k), dev)
+        _require(row_base, "row_base", _U32, (G,), dev)
+        if packed.dtype != torch.uint8 or packed.device != dev or packed.dim() != 2 or \
+                packed.shape[1] != stride or not packed.is_contiguous():
+            raise ValueError(f"packed must be a contiguous uint8 [rows, {stride}] tensor on {dev}")
+        return G, k, stride, row0 & 0xFFFFFFFF
+
+    def unpack_slots(self, packed: torch.Tensor, row_base: torch.Tensor, mask: torch.Tensor,
+                     slots: torch.Tensor, want: int = 1, zero_rest: bool = True, row0: int = 0):
+        """Packed rows -> the selected slots ((mask != 0) == want) of slots [G, k, stride]
+        (ntc_gf256_unpack_slots); row_base [G] u32 = first packed row of each generation.
+        The caller sizes `packed` to hold every selected row (not checked on the device)."""
+        G, k, stride, row0 = self._pack_args(slots, mask, row_base, packed, row0)
+        _native.check(_native.load().ntc_gf256_unpack_slots(
+            self.engine.handle, G, k, stride, packed.data_ptr(), row_base.data_ptr(), row0,
+            mask.data_ptr(), int(bool(want)), slots.data_ptr(), int(bool(zero_rest)),
+            _stream(self.device)), "ntc_gf256_unpack_slots")
+        return slots
+
+    def pack_slots(self, slots: torch.Tensor, mask: torch.Tensor, row_base: torch.Tensor,
+                   packed: torch.Tensor, want: int = 0, row0: int = 0):
+        """Selected slots ((mask != 0) == want) of slots [G, k, stride] -> packed rows
+        (ntc_gf256_pack_slots)."""
+        G, k, stride, row0 = self._pack_args(slots, mask, row_base, packed, row0)
+        _native.check(_native.load().ntc_gf256_pack_slots(
+            self.engine.handle, G, k, stride, slots.data_ptr(), mask.data_ptr(),
+            int(bool(want)), row_base.data_ptr(), row0, packed.data_ptr(),
+            _stream(self.device)), "ntc_gf256_pack_slots")
+        return packed
 
 
 def status_to_numpy(status: torch.Tensor) -> np.ndarray:

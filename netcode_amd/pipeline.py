@@ -172,6 +172,73 @@ class HostPipeline:
                 h_status[g0:g1].copy_(st, non_blocking=True)
         self._join()
 
+    @staticmethod
+    def row_bases(h_mask: torch.Tensor):
+        """(rx_base, lost_base, n_rx, n_lost) for a host mask [G, k]: the first packed row of each
+        generation among the received (mask != 0) and the lost slots, as int32 [G] host tensors."""
+        rx = (h_mask != 0).sum(1, dtype=torch.int64)
+        lost = h_mask.shape[1] - rx
+        rx_base = torch.cumsum(rx, 0) - rx
+        lost_base = torch.cumsum(lost, 0) - lost
+        return (rx_base.to(torch.int32), lost_base.to(torch.int32), int(rx.sum()), int(lost.sum()))
+
+    def encode_decode_packed(self, h_src, h_src_len, h_rep, h_rep_size, h_rx_packed, h_rx_len,
+                             h_mask, h_rmask, h_rec_packed, h_status, sid_base=None,
+                             rid_base=None):
+        """Loopback of one batch moving only the bytes a real sender / receiver pair moves: the
+        sources H2D for the encoder, the repairs D2H; then only the RECEIVED sources H2D, packed
+        (h_rx_packed [n_rx, stride], generation-major, slot order within a generation, as
+        :meth:`row_bases` numbers them), and only the LOST slots D2H, packed (h_rec_packed
+        [n_lost, stride]: the recovered sources, zeros where a generation did not decode --
+        h_status says which).  h_rx_len [G, k] goes in with the received lengths and comes back
+        with the decoded sizes in the lost slots.  Per chunk, the received rows are unpacked into
+        the generation slots on the device (lost slots zeroed), decoded, and the lost slots packed
+        again (ntc_gf256_unpack_slots / ntc_gf256_pack_slots).  Same bytes as encode_decode()."""
+        from .engine import Wire
+        G = h_src.shape[0]
+        self._check(G, h_src=h_src, h_src_len=h_src_len, h_rep=h_rep, h_rep_size=h_rep_size,
+                    h_rx_len=h_rx_len, h_mask=h_mask, h_rmask=h_rmask, h_status=h_status)
+        rx_base, lost_base, n_rx, n_lost = self.row_bases(h_mask)
+        for name, t, n in (("h_rx_packed", h_rx_packed, n_rx), ("h_rec_packed", h_rec_packed, n_lost)):
+            _pinned(t, name)
+            if t.dtype != torch.uint8 or tuple(t.shape) != (n, self.stride):
+                raise ValueError(f"{name} must be uint8 [{n}, {self.stride}], got {t.dtype} {tuple(t.shape)}")
+        sid_base, rid_base = self._bases(G, sid_base, rid_base)
+        wire = Wire(self.device)
+        if not hasattr(self, "d_rows"):
+            self.d_rows = [torch.empty((self.chunk * self.k, self.stride), dtype=torch.uint8,
+                                       device=self.device) for _ in range(self.depth)]
+        d_rx_base = rx_base.to(self.device)
+        d_lost_base = lost_base.to(self.device)
+        self._fork()
+        for s, g0, g1 in self._chunks(G):
+            n = g1 - g0
+            r0, r1 = int(rx_base[g0]), (int(rx_base[g1]) if g1 < G else n_rx)
+            l0, l1 = int(lost_base[g0]), (int(lost_base[g1]) if g1 < G else n_lost)
+            with torch.cuda.stream(self.streams[s]):
+                buf, ln, mk, rmk = self.d_src[s][:n], self.d_len[s][:n], self.d_mask[s][:n], self.d_rmask[s][:n]
+                out, st, rows = self.d_out[s], self.d_status[s][:n], self.d_rows[s]
+                o = EncodeResult(out.repairs[:n], out.encoded_size[:n], out.symbol_len[:n])
+                sid, rid = sid_base[g0:g1], rid_base[g0:g1]
+                buf.copy_(h_src[g0:g1], non_blocking=True)
+                ln.copy_(h_src_len[g0:g1], non_blocking=True)
+                self.enc[s](buf, ln, sid, rid, o)
+                h_rep[g0:g1].copy_(o.repairs, non_blocking=True)
+                h_rep_size[g0:g1].copy_(o.encoded_size, non_blocking=True)
+                for d, h in ((ln, h_rx_len), (mk, h_mask), (rmk, h_rmask)):
+                    d.copy_(h[g0:g1], non_blocking=True)
+                rows[:r1 - r0].copy_(h_rx_packed[r0:r1], non_blocking=True)
+                # the decoder's slots reuse the source buffer (stream order: the encode has read it)
+                wire.unpack_slots(rows[:max(r1 - r0, 1)], d_rx_base[g0:g1], mk, buf, want=1,
+                                  zero_rest=True, row0=r0)
+                self.dec[s](buf, ln, mk, o.repairs, o.encoded_size, rmk, sid, rid, st)
+                if l1 > l0:
+                    wire.pack_slots(buf, mk, d_lost_base[g0:g1], rows[:l1 - l0], want=0, row0=l0)
+                    h_rec_packed[l0:l1].copy_(rows[:l1 - l0], non_blocking=True)
+                h_rx_len[g0:g1].copy_(ln, non_blocking=True)
+                h_status[g0:g1].copy_(st, non_blocking=True)
+        self._join()
+
     def encode_decode(self, h_src, h_src_len, h_rep, h_rep_size, h_rx, h_rx_len, h_mask, h_rmask,
                       h_status, sid_base=None, rid_base=None):
         """Loopback of one batch (bench.py's host-resident rate): per chunk, sources H2D -> encode

@@ -90,6 +90,59 @@ def test_pipeline_matches_oracle(gpu, G, chunk, depth, explicit_ids):
     assert (h_rx2.numpy() == oout).all()
     assert (h_rxlen2.numpy().view(np.uint16) == olen).all()
 
+    # loopback moving only received rows in and lost rows out (packed)
+    h_mask = pinned(mask)
+    _, _, n_rx, n_lost = HostPipeline.row_bases(h_mask)
+    assert n_rx == int(mask.sum()) and n_lost == mask.size - n_rx
+    h_rxp = pinned(src[mask != 0])
+    h_rec = torch.full((n_lost, S), 0xAB, dtype=torch.uint8).pin_memory()
+    h_rep3 = torch.zeros((G, r, S), dtype=torch.uint8).pin_memory()
+    h_rsz3 = torch.zeros((G, r), dtype=torch.int16).pin_memory()
+    h_st3 = torch.zeros((G, 12), dtype=torch.uint8).pin_memory()
+    h_rxlen3 = pinned(llen)
+    p.encode_decode_packed(pinned(src), pinned(lens), h_rep3, h_rsz3, h_rxp, h_rxlen3, h_mask,
+                           pinned(rmask), h_rec, h_st3, d_sid, d_rid)
+    torch.cuda.synchronize(gpu)
+    assert (h_rep3.numpy() == orep).all()
+    assert (status_to_numpy(h_st3) == ost).all()
+    assert (h_rxlen3.numpy().view(np.uint16) == olen).all()
+    # lost slots, packed in (generation, slot) order: the oracle's recovered bytes (zeros where
+    # the oracle left the slot untouched, i.e. the zeroed lost slot)
+    assert (h_rec.numpy() == oout[mask == 0]).all()
+
+
+@pytest.mark.parametrize("k,stride,want,zero_rest", [(24, 64, 1, True), (300, 32, 0, False),
+                                                     (7, 4096, 1, False)])
+def test_pack_unpack_slots(gpu, k, stride, want, zero_rest):
+    """ntc_gf256_unpack_slots / ntc_gf256_pack_slots against numpy boolean indexing, with a
+    chunk-relative packed buffer (row0) and generations with no selected slot."""
+    import torch
+    from netcode_amd import Wire
+    rng = np.random.default_rng(k + stride)
+    G = 11
+    mask = (rng.random((G, k)) < 0.6).astype(np.uint8) * rng.integers(1, 256, (G, k), dtype=np.uint8)
+    mask[3] = 0
+    mask[5] = 1
+    sel = (mask != 0) == bool(want)
+    cnt = sel.sum(1)
+    base = np.cumsum(cnt) - cnt + 5                      # rows numbered from row0 = 5
+    n = int(cnt.sum())
+    packed = rng.integers(0, 256, (max(n, 1), stride), dtype=np.uint8)
+    slots0 = rng.integers(0, 256, (G, k, stride), dtype=np.uint8)
+    w = Wire(gpu)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    d_slots = d(slots0)
+    d_mask, d_base = d(mask), d(base.astype(np.int32))
+    w.unpack_slots(d(packed), d_base, d_mask, d_slots, want=want, zero_rest=zero_rest, row0=5)
+    exp = slots0.copy()
+    exp[sel] = packed[:n]
+    if zero_rest:
+        exp[~sel] = 0
+    assert (d_slots.cpu().numpy() == exp).all()
+    out = d(np.zeros((max(n, 1), stride), np.uint8))
+    w.pack_slots(d(slots0), d_mask, d_base, out, want=want, row0=5)
+    assert (out.cpu().numpy()[:n] == slots0[sel]).all()
+
 
 def test_pipeline_rejects_bad_shapes(gpu):
     """Host tensors of the wrong dtype / trailing shape raise instead of being cast or broadcast

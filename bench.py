@@ -49,7 +49,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=40)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--config", default="k128r32s4096", choices=sorted(CONFIGS))
     p.add_argument("--G", type=int, default=0, help="generations per GPU (default per config)")
     p.add_argument("--mixed", action="store_true", help="m ~ U[0, r] instead of m = r")
@@ -435,6 +435,44 @@ def per_packet_main(a):
         sys.exit(3)
 
 
+def cpu_baseline_dense(w, sample_bytes=1024):
+    """Config 5 CPU leg: the oracle's dense encode (region MACs, AVX2 split-nibble) and dense
+    decode (the reference's jerasure-order Gauss-Jordan, invert_matrix.cc:9-128, then the MACs
+    with the inverse) on the bench's own matrix, single core.  The MACs run over a `sample_bytes`
+    column slice of the 64 KiB sources and scale linearly in S (the per-byte work of every MAC is
+    the same); the inversion runs once, in full.  value = k*S / (t_enc_mac(S) + t_invert +
+    t_dec_mac(S))."""
+    from oracle import oracle as O
+    L = O.lib()
+    L.or_set_simd(1)
+    try:
+        mat = w.mat[0].cpu().numpy()
+        src = np.ascontiguousarray(w.src[0, :, :sample_bytes].cpu().numpy())
+        t0 = time.perf_counter()
+        rep = O.dense_encode(mat, src)
+        t1 = time.perf_counter()
+        ok, out, inv = O.dense_decode(mat, rep)
+        t2 = time.perf_counter()
+        again = O.dense_encode(inv, rep)          # the decode's MAC alone (same matrix, same rows)
+        t3 = time.perf_counter()
+    finally:
+        L.or_set_simd(0)
+    t_enc, t_dmac = t1 - t0, t3 - t2
+    t_inv = max(t2 - t1 - t_dmac, 0.0)
+    fail = None if (again == src).all() else "mismatch"
+    scale = w.S / sample_bytes
+    total = t_enc * scale + t_inv + t_dmac * scale
+    model, nproc, usable = cpu_info()
+    return {"value": round(w.k * w.S / total / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"k={w.k} dense: encode + decode MACs over a {sample_bytes}-byte column "
+                      f"slice scaled x{scale:g} to S={w.S}, plus one full {w.k}x{w.k} inversion "
+                      f"(oracle, jerasure order); {t3 - t0:.1f}s wall",
+            "encode_mac_s_at_S": round(t_enc * scale, 3), "invert_s": round(t_inv, 3),
+            "decode_mac_s_at_S": round(t_dmac * scale, 3),
+            "sample_bit_exact": bool(ok and fail is None and (out == src).all()),
+            "cpu_model": model, "nproc": nproc, "usable_cpus": usable}
+
+
 def kernel_summary(log, steps, dense):
     """Per-step kernel times from the timing log of the timed steps: {name: ms per step} and the
     per-launch durations of the encode / decode MAC kernels."""
@@ -471,8 +509,10 @@ def pmc_record(fname, config, kernel):
     rec = j.get(config, {}).get(kernel)
     if rec is None:
         return None, None
-    src = {"file": "profiles/" + fname, "commit": j.get("_commit", "unrecorded"),
-           "how": j.get("_how", "rocprofv3 --pmc passes")}
+    ent = j.get(config, {})
+    src = {"file": "profiles/" + fname,
+           "commit": ent.get("_commit", j.get("_commit", "unrecorded")),
+           "how": ent.get("_how", j.get("_how", "rocprofv3 --pmc passes"))}
     return rec, src
 
 
@@ -503,7 +543,7 @@ def main():
     if dense:
         w = DenseWorkload(dev, G, k, S, rank)
         engine = w.dc.engine
-        a.no_host_rate = a.no_cpu_baseline = True
+        a.no_host_rate = True
     else:
         w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
         engine = w.enc.engine
@@ -596,7 +636,8 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         _, _, usable = cpu_info()
         thr = a.cpu_threads or min(16, usable)
-        line["cpu_baseline"] = cpu_baseline(k, r, S, stride, m, thr)
+        line["cpu_baseline"] = (cpu_baseline_dense(w) if dense
+                                else cpu_baseline(k, r, S, stride, m, thr))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

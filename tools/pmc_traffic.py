@@ -15,8 +15,22 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOW = "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --steps 2 --warmup 1 (tools/gpu_pmc.sh)"
 KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
            "decode_mac": (r"gf_mac_bj<\d+, true", r"gf_mac<\d, true")}
+
+
+def git_head():
+    """The commit the measured tree was sent from (gpurun snapshots this working tree)."""
+    import subprocess
+    try:
+        h = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                           text=True, check=True).stdout.strip()
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+                               capture_output=True, text=True).stdout.strip()
+        return h + ("+dirty" if dirty else "")
+    except (OSError, subprocess.CalledProcessError):
+        return "unknown"
 
 
 def means(path, counter):
@@ -51,6 +65,8 @@ def main():
                                 "FETCH_SIZE_KiB_raw": f, "WRITE_SIZE_KiB": w}
     ent["note"] = ("bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024); FETCH_SIZE doubled "
                    "per the gfx950 correction")
+    ent["_commit"] = git_head()
+    ent["_how"] = HOW
     out[cfg] = ent
     json.dump(out, open(out_p, "w"), indent=1)
     print(json.dumps(ent, indent=1))

@@ -20,7 +20,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
            "decode_mac": (r"gf_mac_bj<\d+, true", r"gf_mac<\d, true")}
-CONFIGS = {"k128r32s4096": (128, 32, 4096, 4096, 32)}   # k, r, S, G, m
+CONFIGS = {"k128r32s4096": (128, 32, 4096, 4096, 32),   # k, r, S, G, m
+           "k32r8s1024": (32, 8, 1024, 4096, 8), "k128r32s1500": (128, 32, 1500, 8192, 32)}
+HOW = "rocprofv3 --pmc, 2 SQ passes of bench.py --steps 2 --warmup 1 (tools/gpu_pmc.sh)"
+
+
+def git_head():
+    """The commit the measured tree was sent from (gpurun snapshots this working tree)."""
+    import subprocess
+    try:
+        h = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                           text=True, check=True).stdout.strip()
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+                               capture_output=True, text=True).stdout.strip()
+        return h + ("+dirty" if dirty else "")
+    except (OSError, subprocess.CalledProcessError):
+        return "unknown"
 
 
 def means(paths):
@@ -53,6 +68,8 @@ def main():
                                   "wait_waitcnt": round(cs["SQ_WAIT_ANY"] / wc, 3),
                                   "issue_stall": round(cs["SQ_WAIT_INST_ANY"] / wc, 3)},
         }
+    ent["_commit"] = git_head()
+    ent["_how"] = HOW
     out[cfg] = ent
     out["note"] = ("SQ PMC passes (tools/gpu_sq.sh, tools/pmc_valu.py); VALU issue slots = 1024 SIMDs x "
                    "(GRBM_GUI_ACTIVE/8) / 2 cycles per wave64 VALU op")

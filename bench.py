@@ -9,9 +9,11 @@ Multi-GPU (torchrun): every rank owns G independent generations with its own id 
 scaling, no data-path collective); only a barrier and a max-reduce of the timing use RCCL.
 
 Extras in the JSON line:
-* kernels_ms / roofline: every kernel of the TIMED steps is bracketed by a HIP event pair on its
-  launch stream (engine timing log, ntc_gf256_timing_log), so the per-step kernel sums and the
-  dominant MAC kernel's duration come from the very launches the step time covers;
+* roofline: every MAC kernel of the TIMED steps is bracketed by a HIP event pair on its launch
+  stream (engine timing log, ntc_gf256_timing_log restricted to the MAC kinds), so the dominant
+  kernel's duration comes from the very launches the step time covers; kernels_ms = every kernel
+  of a separate, untimed pass of the same steps with all launches bracketed (each logged launch
+  costs two event records, microseconds that would distort sub-millisecond steps);
 * roofline.traffic / valu_profile: HBM bytes and SQ instruction counts of the same kernel from
   separate rocprofv3 --pmc passes (they cannot run inside this process), labelled with the file
   and the commit they were measured at;
@@ -559,7 +561,7 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
     # every kernel of the timed steps gets an event pair on its launch stream (engine timing log)
-    engine.timing_log(a.steps * 16)
+    engine.timing_log(a.steps * 16, kinds=("encode_mac", "decode_mac"))
     t0 = time.perf_counter()
     for _ in range(a.steps):
         w.step()
@@ -579,7 +581,18 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     payload = G * k * S * world
     value = payload / (elapsed / a.steps) / 2**30
-    kern, launches = kernel_summary(log, a.steps, dense)
+    _, launches = kernel_summary(log, a.steps, dense)
+    # per-kernel breakdown: a separate pass with every launch bracketed (not the timed steps)
+    nb = min(a.steps, 10)
+    torch.cuda.synchronize(dev)
+    engine.timing_log(nb * 16)
+    tb = time.perf_counter()
+    for _ in range(nb):
+        w.step()
+    torch.cuda.synchronize(dev)
+    ms_logged = (time.perf_counter() - tb) / nb * 1e3
+    kern, _ = kernel_summary(engine.timing_read(), nb, dense)
+    engine.timing_log(0)
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / its mean launch duration
     # over the timed steps.  Encode MAC: read k*S, write r*S per generation; decode MAC: per
@@ -620,7 +633,9 @@ def main():
                           "coefficient schedule (encoded and planned, no decode MAC)",
             "roofline": roof,
             "kernels_ms": {n: round(v, 4) for n, v in sorted(kern.items())},
-            "kernels_ms_note": "per timed step, summed over that step's launches",
+            "kernels_ms_note": f"per step, summed over that step's launches; from {nb} extra "
+                               f"untimed steps with every launch bracketed by events "
+                               f"({ms_logged:.4f} ms per step there)",
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_step),
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}

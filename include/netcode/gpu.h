@@ -92,11 +92,15 @@ int  ntc_gf256_mac_time(ntc_gf256_engine* eng, int dec, float* ms);
  * turns the log off; every call clears it).  ntc_gf256_timing_read waits for the logged kernels
  * and returns up to `max` entries in launch order: kinds[i] (NTC_GF256_K_*) and ms[i] (that
  * kernel's duration); *n = entries logged.  bench.py times the kernels of its timed steps this
- * way, so per-step kernel sums come from the same launches as the step time. */
+ * way, so per-step kernel sums come from the same launches as the step time.
+ * ntc_gf256_timing_kinds restricts the log to the kinds whose bit (1 << NTC_GF256_K_*) is set in
+ * `mask` (default: all): every logged kernel costs two event records on its stream, a few
+ * microseconds that matter for sub-millisecond steps. */
 enum { NTC_GF256_K_ENCODE_PREP = 0, NTC_GF256_K_ENCODE_MAC = 1, NTC_GF256_K_DECODE_PLAN = 2,
        NTC_GF256_K_PLAN_ROWS = 3, NTC_GF256_K_DECODE_MAC = 4, NTC_GF256_K_BJ_OFFSETS = 5,
        NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 };
 int  ntc_gf256_timing_log(ntc_gf256_engine* eng, uint32_t capacity);
+int  ntc_gf256_timing_kinds(ntc_gf256_engine* eng, uint32_t mask);
 int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uint32_t* kinds,
                            float* ms);
 

@@ -25,7 +25,7 @@ GPU_H_SYMBOLS = [
     "ntc_gf256_read_packets", "ntc_gf256_unpack_slots", "ntc_gf256_pack_slots",
     "ntc_gf_combine_batch", "ntc_gf_region_multiply", "ntc_gf_coefficient", "ntc_gf_multiply",
     "ntc_gf_invert", "ntc_gf_multiply_size", "ntc_gf256_set_timing", "ntc_gf256_mac_time",
-    "ntc_gf256_set_plan_kind", "ntc_gf256_timing_log", "ntc_gf256_timing_read",
+    "ntc_gf256_set_plan_kind", "ntc_gf256_timing_log", "ntc_gf256_timing_read", "ntc_gf256_timing_kinds",
 ]
 
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "EUNSUPPORTED"}
@@ -95,6 +95,7 @@ def load(path: str | None = None):
     L.ntc_gf256_mac_time.argtypes = [V, C.c_int, C.POINTER(C.c_float)]
     L.ntc_gf256_set_plan_kind.argtypes = [V, C.c_int]
     L.ntc_gf256_timing_log.argtypes = [V, u32]
+    L.ntc_gf256_timing_kinds.argtypes = [V, u32]
     L.ntc_gf256_timing_read.argtypes = [V, u32, C.POINTER(u32), P, P]
     L.ntc_gf_combine_batch.argtypes = [V, u32, u32, u32, u32, u32, P, P, P, V]
     L.ntc_gf_region_multiply.argtypes = [V, u32, P, P, C.c_size_t, u32, C.c_int, V]

@@ -34,6 +34,7 @@ struct ntc_gf256_engine {
   hipEvent_t mac_ev[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   // kernel timing log (ntc_gf256_timing_log): an event pair around every launch, in launch order
   uint32_t tlog_cap = 0, tlog_n = 0;
+  uint32_t tlog_mask = ~0u;            // bit k: log kernels of kind k (ntc_gf256_timing_kinds)
   std::vector<hipEvent_t> tlog_ev;     // 2 per entry
   std::vector<uint32_t> tlog_kind;     // NTC_GF256_K_*
   // geometry of the last plan (decode_apply must match)
@@ -67,7 +68,7 @@ class KernelTimer {
  public:
   KernelTimer(ntc_gf256_engine* e, uint32_t kind, hipStream_t st) : e_(e), st_(st)
   {
-    if (e_->tlog_n < e_->tlog_cap) {
+    if (e_->tlog_n < e_->tlog_cap && ((e_->tlog_mask >> kind) & 1u)) {
       slot_ = static_cast<int>(e_->tlog_n++);
       e_->tlog_kind[slot_] = kind;
       (void)hipEventRecord(e_->tlog_ev[2 * slot_], st_);

@@ -2281,6 +2281,13 @@ int ntc_gf256_timing_log(ntc_gf256_engine* e, uint32_t capacity)
   return NTC_GPU_OK;
 }
 
+int ntc_gf256_timing_kinds(ntc_gf256_engine* e, uint32_t mask)
+{
+  if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
+  e->tlog_mask = mask;
+  return NTC_GPU_OK;
+}
+
 int ntc_gf256_timing_read(ntc_gf256_engine* e, uint32_t max, uint32_t* n, uint32_t* kinds, float* ms)
 {
   if (!e || !n || (max && (!kinds || !ms))) return fail(NTC_GPU_EINVAL, "NULL argument");

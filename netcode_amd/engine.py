@@ -112,8 +112,11 @@ class Engine:
     KERNEL_KINDS = ("encode_prep", "encode_mac", "decode_plan", "plan_rows", "decode_mac",
                     "bj_offsets", "dense", "other")
 
-    def timing_log(self, capacity: int):
-        """Bracket each of the next `capacity` kernel launches with HIP events (0 = off)."""
+    def timing_log(self, capacity: int, kinds=None):
+        """Bracket each of the next `capacity` kernel launches with HIP events (0 = off);
+        `kinds` (names of KERNEL_KINDS) restricts the log to those kernels (None = all)."""
+        mask = 0xFFFFFFFF if kinds is None else sum(1 << Engine.KERNEL_KINDS.index(k) for k in kinds)
+        _native.check(self._L.ntc_gf256_timing_kinds(self._h, mask), "ntc_gf256_timing_kinds")
         _native.check(self._L.ntc_gf256_timing_log(self._h, int(capacity)), "ntc_gf256_timing_log")
 
     def timing_read(self, max_entries: int = 1 << 16):

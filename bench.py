@@ -12,8 +12,8 @@ Extras in the JSON line:
 * roofline: every MAC kernel of the TIMED steps is bracketed by a HIP event pair on its launch
   stream (engine timing log, ntc_gf256_timing_log restricted to the MAC kinds), so the dominant
   kernel's duration comes from the very launches the step time covers; kernels_ms = every kernel
-  of a separate, untimed pass of the same steps with all launches bracketed (each logged launch
-  costs two event records, microseconds that would distort sub-millisecond steps);
+  of the last 10 warmup steps, run with all launches bracketed (each logged launch costs two
+  event records, microseconds that would distort sub-millisecond timed steps);
 * roofline.traffic / valu_profile: HBM bytes and SQ instruction counts of the same kernel from
   separate rocprofv3 --pmc passes (they cannot run inside this process), labelled with the file
   and the commit they were measured at;
@@ -550,8 +550,23 @@ def main():
         w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
         engine = w.enc.engine
 
-    for _ in range(a.warmup):
+    # the last nb warmup steps run with every kernel bracketed by events (kernels_ms breakdown);
+    # the timed steps then log only the MAC kernels (roofline), in the same log
+    nb = min(a.warmup, 10)
+    for i in range(a.warmup):
+        if i == a.warmup - nb:
+            torch.cuda.synchronize(dev)
+            engine.timing_log((nb + a.steps) * 16)
+            tb = time.perf_counter()
         w.step()
+    torch.cuda.synchronize(dev)
+    if nb:
+        ms_logged = (time.perf_counter() - tb) / nb * 1e3
+        n_breakdown = len(engine.timing_read())
+        engine.timing_kinds(("encode_mac", "decode_mac"))
+    else:
+        ms_logged, n_breakdown = 0.0, 0
+        engine.timing_log(a.steps * 16, kinds=("encode_mac", "decode_mac"))
 
     def barrier():
         if world > 1:
@@ -560,16 +575,16 @@ def main():
 
     barrier()
     torch.cuda.synchronize(dev)
-    # every kernel of the timed steps gets an event pair on its launch stream (engine timing log)
-    engine.timing_log(a.steps * 16, kinds=("encode_mac", "decode_mac"))
+    # every MAC kernel of the timed steps gets an event pair on its launch stream (timing log)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         w.step()
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    log = engine.timing_read()
+    full_log = engine.timing_read()
     engine.timing_log(0)
+    log = full_log[n_breakdown:]
     # outputs of the timed steps, checked after the clock stops (warmup runs straight into the
     # timed loop, with no host-side check idling the GPU between them)
     good, ndec, dec_bytes, dec_macs = w.verify()
@@ -582,17 +597,7 @@ def main():
     payload = G * k * S * world
     value = payload / (elapsed / a.steps) / 2**30
     _, launches = kernel_summary(log, a.steps, dense)
-    # per-kernel breakdown: a separate pass with every launch bracketed (not the timed steps)
-    nb = min(a.steps, 10)
-    torch.cuda.synchronize(dev)
-    engine.timing_log(nb * 16)
-    tb = time.perf_counter()
-    for _ in range(nb):
-        w.step()
-    torch.cuda.synchronize(dev)
-    ms_logged = (time.perf_counter() - tb) / nb * 1e3
-    kern, _ = kernel_summary(engine.timing_read(), nb, dense)
-    engine.timing_log(0)
+    kern = kernel_summary(full_log[:n_breakdown], nb, dense)[0] if nb else {}   # logged warmup
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / its mean launch duration
     # over the timed steps.  Encode MAC: read k*S, write r*S per generation; decode MAC: per
@@ -633,8 +638,8 @@ def main():
                           "coefficient schedule (encoded and planned, no decode MAC)",
             "roofline": roof,
             "kernels_ms": {n: round(v, 4) for n, v in sorted(kern.items())},
-            "kernels_ms_note": f"per step, summed over that step's launches; from {nb} extra "
-                               f"untimed steps with every launch bracketed by events "
+            "kernels_ms_note": f"per step, summed over that step's launches; from the last {nb} "
+                               f"warmup steps, run with every launch bracketed by events "
                                f"({ms_logged:.4f} ms per step there)",
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_step),

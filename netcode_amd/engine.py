@@ -115,9 +115,13 @@ class Engine:
     def timing_log(self, capacity: int, kinds=None):
         """Bracket each of the next `capacity` kernel launches with HIP events (0 = off);
         `kinds` (names of KERNEL_KINDS) restricts the log to those kernels (None = all)."""
+        self.timing_kinds(kinds)
+        _native.check(self._L.ntc_gf256_timing_log(self._h, int(capacity)), "ntc_gf256_timing_log")
+
+    def timing_kinds(self, kinds=None):
+        """Restrict the running log to `kinds` from now on (None = all); logged entries stay."""
         mask = 0xFFFFFFFF if kinds is None else sum(1 << Engine.KERNEL_KINDS.index(k) for k in kinds)
         _native.check(self._L.ntc_gf256_timing_kinds(self._h, mask), "ntc_gf256_timing_kinds")
-        _native.check(self._L.ntc_gf256_timing_log(self._h, int(capacity)), "ntc_gf256_timing_log")
 
     def timing_read(self, max_entries: int = 1 << 16):
         """[(kernel kind name, ms)] of the logged launches, in launch order (waits for them)."""

@@ -1125,6 +1125,66 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
       }
       if (!singular) { ok = true; break; }
       __syncthreads();
+      if (t == m - 1 && t + 1 < nrecv) {
+        // The first candidate failed.  Rather than a full Gauss-Jordan per further candidate
+        // (decoder.cc:448-468 tries t = m, m+1, ... in turn), screen them all at once, as
+        // decode_plan_big does: {first m-1 repairs} + {t} is invertible iff the first m-1 rows
+        // are independent and row t lies outside their span.  Forward elimination of all
+        // received rows over the m missing columns with pivots from rows 0..m-2 only leaves
+        // each candidate reduced against that basis; the first nonzero one is the repair the
+        // reference stops at (none: every candidate fails).
+        const uint32_t nwl = (m + 3) / 4;
+        if (lane < nrecv) {
+          const uint32_t rid = ridb + recv[lane];
+          for (uint32_t w = 0; w < nwl; ++w) {
+            uint32_t word = 0;
+            for (uint32_t b = 0; b < 4; ++b) {
+              const uint32_t c = 4 * w + b;
+              if (c < m) word |= coefficient(rid, sidb + miss[c]) << (8 * b);
+            }
+            A[lane][w] = word;
+          }
+        }
+        __syncthreads();
+        uint32_t rank = 0;
+        for (uint32_t c = 0; c < m && rank + 1 < m; ++c) {
+          const uint32_t cw = c >> 2, cs = 8 * (c & 3);
+          const uint32_t f = lane < nrecv ? (A[lane][cw] >> cs) & 0xFFu : 0u;
+          const uint64_t b = __ballot(lane >= rank && lane + 1 < m && f != 0);
+          if (b == 0) continue;                       // no pivot in this column (uniform)
+          const uint32_t q = __ffsll(static_cast<unsigned long long>(b)) - 1;
+          if (q != rank) {
+            for (uint32_t w = lane; w < nwl; w += 64) {
+              const uint32_t tmp = A[rank][w];
+              A[rank][w] = A[q][w];
+              A[q][w] = tmp;
+            }
+            __syncthreads();
+          }
+          const uint32_t* ti = d_perm.w[field_inv_dev((A[rank][cw] >> cs) & 0xFFu)];
+          for (uint32_t w = lane; w < nwl; w += 64) A[rank][w] = mul4(ti, A[rank][w]);
+          __syncthreads();
+          const uint32_t fa = (lane > rank && lane < nrecv) ? (A[lane][cw] >> cs) & 0xFFu : 0u;
+          if (fa != 0) {
+            uint32_t tf[5];
+#pragma unroll
+            for (int e = 0; e < 5; ++e) tf[e] = d_perm.w[fa][e];
+            for (uint32_t w = 0; w < nwl; ++w) A[lane][w] ^= mul4(tf, A[rank][w]);
+          }
+          __syncthreads();
+          ++rank;
+        }
+        uint32_t next = nrecv;                        // none: every candidate fails
+        if (rank + 1 == m) {
+          uint32_t nz = 0;
+          if (lane + 1 >= m && lane < nrecv)
+            for (uint32_t w = 0; w < nwl; ++w) nz |= A[lane][w];
+          const uint64_t b = __ballot(nz != 0);
+          if (b != 0) next = __ffsll(static_cast<unsigned long long>(b)) - 1;
+        }
+        __syncthreads();
+        t = next - 1;                                 // the loop's ++t moves to `next`
+      }
     }
     if (!ok) {
       st.state = 3;

@@ -145,6 +145,10 @@ DECODE_CASES = [
     (9, 33, 12, 2080, 2080, "exact", 12, True),       # odd k (unaligned plan rows), 8+4 row tiles
     (30, 7, 5, 4096, 4096, "iid", 0.3, False),        # tiny k, mixed outcomes
     (12, 45, 24, 2048, 2048, "mixed", 24, False),     # k % 4 != 0, 1-3 row tiles per generation
+    # iid loss of sources and repairs, r > 32: a few generations decode only after the first
+    # candidate repair fails (decoder.cc:448-468 retry; the LDS plan's rank screening)
+    (400, 100, 64, 64, 64, "iid", 0.35, False),
+    (400, 60, 40, 64, 64, "iid", 0.3, True),
 ]
 
 

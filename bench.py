@@ -550,6 +550,10 @@ def main():
         w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
         engine = w.enc.engine
 
+    # optional: the HBM copy probe (reported in the roofline) before the warmup steps, with more
+    # repetitions (clock ramp experiment, NTC_BENCH_PROBE_FIRST=<reps>)
+    probe_reps = int(os.environ.get("NTC_BENCH_PROBE_FIRST", "0"))
+    probe = hbm_copy_probe(dev, reps=probe_reps) if probe_reps else None
     # the last nb warmup steps run with every kernel bracketed by events (kernels_ms breakdown);
     # the timed steps then log only the MAC kernels (roofline), in the same log
     nb = min(a.warmup, 10)
@@ -623,7 +627,7 @@ def main():
             "byte_macs_per_launch": int(macs),
             "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2),
             "valu_profile": valu, "valu_profile_source": vsrc,
-            "hbm_copy_probe_GBps": hbm_copy_probe(dev)}
+            "hbm_copy_probe_GBps": probe if probe is not None else hbm_copy_probe(dev)}
 
     line = {"metric": "device-resident GF(256) encode+decode GiB/s, k=128 r=32, 4 KiB pkts, 1/2/4/8 GPU",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,

@@ -21,12 +21,16 @@ KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
 
 
 def git_head():
-    """The commit the measured tree was sent from (gpurun snapshots this working tree)."""
+    """The commit the measured tree was sent from (gpurun snapshots this working tree);
+    NTC_PMC_COMMIT overrides it when the counters are processed after later commits."""
     import subprocess
+    if os.environ.get("NTC_PMC_COMMIT"):
+        return os.environ["NTC_PMC_COMMIT"]
     try:
         h = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
                            text=True, check=True).stdout.strip()
-        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no", "--",
+                                ".", ":!profiles"],
                                capture_output=True, text=True).stdout.strip()
         return h + ("+dirty" if dirty else "")
     except (OSError, subprocess.CalledProcessError):

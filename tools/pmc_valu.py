@@ -26,12 +26,16 @@ HOW = "rocprofv3 --pmc, 2 SQ passes of bench.py --steps 2 --warmup 1 (tools/gpu_
 
 
 def git_head():
-    """The commit the measured tree was sent from (gpurun snapshots this working tree)."""
+    """The commit the measured tree was sent from (gpurun snapshots this working tree);
+    NTC_PMC_COMMIT overrides it when the counters are processed after later commits."""
     import subprocess
+    if os.environ.get("NTC_PMC_COMMIT"):
+        return os.environ["NTC_PMC_COMMIT"]
     try:
         h = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
                            text=True, check=True).stdout.strip()
-        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no"],
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no", "--",
+                                ".", ":!profiles"],
                                capture_output=True, text=True).stdout.strip()
         return h + ("+dirty" if dirty else "")
     except (OSError, subprocess.CalledProcessError):

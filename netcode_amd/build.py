@@ -65,6 +65,7 @@ OUT_DIR = os.path.join(ROOT, "tests", "_build")
 # from /root/reference; every netcode/ header they include resolves to include/ (this repo).
 CPP_CHECKS = {
     "cpp_surface_test": (["tests/cpp/cpp_surface_test.cc"], False),
+    "detail_packetizer_test": (["tests/cpp/detail_packetizer_test.cc"], False),
     "ref_cpp_basic": ([REF + "/examples/basic/cpp_basic.cc"], True),
     "ref_c_basic": ([REF + "/examples/basic/c_basic.c"], True),
     "ref_end_to_end": ([REF + "/tests/end_to_end.cc"], True),

@@ -35,3 +35,12 @@ def test_no_device_fails_loudly(cpp_checks):
     r = subprocess.run([cpp_checks["cpp_surface_test"], "10"], capture_output=True, text=True, timeout=60)
     assert r.returncode != 0
     assert "no MI355X engine" in r.stderr
+
+
+def test_detail_packetizer_cases(cpp_checks):
+    """The detail-layer packetizer (include/netcode/detail/packetizer.hh) on the cases of the
+    reference's test_packetizer.cc (not buildable here: Boost.Endian) plus the SURVEY §8(c) wire
+    KAT; header-only, runs on the CPU."""
+    r = subprocess.run([cpp_checks["detail_packetizer_test"]], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout

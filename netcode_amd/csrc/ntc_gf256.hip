@@ -164,7 +164,6 @@ struct MacArgs {
   const uint8_t* coef;         // [G][k][rp] coefficient bytes, row-minor
   uint32_t rp;
   const uint32_t* joff;        // bit-sliced kernel: block offsets [G][k][ntiles][16]
-  uint32_t row_ptr_g0;         // host: first row_ptr entry (in generations) this launch uses
   uint32_t ntiles;
   const uint64_t* row_ptr;     // bit-sliced decode: input row address per plan position,
                                // [G][k + kBjRing] (plan_rows; the tail repeats position k-1)
@@ -2054,17 +2053,17 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
                  : (dec ? gf_mac_bj<8, true, 0, 1> : gf_mac_bj<8, false, 0, 1>);
     a.ntiles = (a.rows + 7) / 8;
     if (dec) {
-      const uint64_t nr = static_cast<uint64_t>(a.row_ptr_g0 + a.G) * (a.k + kBjRing);
+      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
       if (rc) return rc;
       {
         KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
         hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
                            a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
-                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr) + static_cast<size_t>(a.row_ptr_g0) * (a.k + kBjRing));
+                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
       }
       if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
-      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr) + static_cast<size_t>(a.row_ptr_g0) * (a.k + kBjRing);
+      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
     }
     if (gv == 1) {
       const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles;
@@ -2090,17 +2089,17 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
                   : (dec ? gf_mac_bj<8, true> : gf_mac_bj<8, false>);
     a.ntiles = (a.rows + rt - 1) / rt;
     if (dec) {   // input row addresses of the plan positions (MacArgs::row_ptr)
-      const uint64_t nr = static_cast<uint64_t>(a.row_ptr_g0 + a.G) * (a.k + kBjRing);
+      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
       if (rc) return rc;
       {
         KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
         hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
                            a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
-                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr) + static_cast<size_t>(a.row_ptr_g0) * (a.k + kBjRing));
+                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
       }
       if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
-      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr) + static_cast<size_t>(a.row_ptr_g0) * (a.k + kBjRing);
+      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
     }
     const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 2u * rt;
     if (offsets_ready && rt == 8) {
@@ -2426,15 +2425,13 @@ static int encode_part(ntc_gf256_engine* e, uint32_t g0, uint32_t Gh, uint32_t k
 // engine's side stream); NTC_GF256_SPLIT=0 turns this off (A/B runs).
 constexpr uint32_t kSplitMin = 512;
 
-static bool split_batches(const ntc_gf256_engine* e, uint32_t stride)
+static bool split_batches()
 {
   static const bool on = [] {
     const char* v = std::getenv("NTC_GF256_SPLIT");
     return !(v && std::atoi(v) == 0);
   }();
-  // the halves' MACs run concurrently: only MAC paths without a shared jump-offset scratch
-  // (v_perm, or the shared-table chains that read coefficient bytes)
-  return on && (!use_bitslice(e, stride) || gx_chain() >= 2);
+  return on;
 }
 
 static int ensure_side(ntc_gf256_engine* e)
@@ -2506,10 +2503,10 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
     rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   }
   if (rc) return rc;
-  if (G < kSplitMin || !split_batches(e, stride))
+  if (G < kSplitMin || !split_batches())
     return encode_part(e, 0, G, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
                        rep_len, st, fused, true, true);
-  // prep A; then [MAC A on st | prep B, MAC B on side]; st joins the side stream
+  // prep A; [MAC A on st | prep B on side]; MAC B on st after both
   const uint32_t GA = G / 2, GB = G - GA;
   if ((rc = presize_mac(e, false, G, k, r, stride))) return rc;
   if ((rc = encode_part(e, 0, GA, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
@@ -2517,12 +2514,14 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
     return rc;
   if ((rc = fork_side(e, st))) return rc;
   if ((rc = encode_part(e, GA, GB, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
-                        rep_len, e->side, fused, true, true)))
+                        rep_len, e->side, fused, true, false)))
     return rc;
   if ((rc = encode_part(e, 0, GA, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
                         rep_len, st, fused, false, true)))
     return rc;
-  return join_side(e, st);
+  if ((rc = join_side(e, st))) return rc;
+  return encode_part(e, GA, GB, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
+                     rep_len, st, fused, false, true);
 }
 
 // Plan of generations [g0, g0 + G) of a batch of Gall generations (pointers are the batch's).
@@ -2639,7 +2638,6 @@ static int apply_part(ntc_gf256_engine* e, uint32_t g0, uint32_t G, uint32_t k, 
   a.rows_per_gen = e->plan_m + g0; a.in_idx = e->plan_in + gk;
   a.out_idx = e->plan_out + static_cast<size_t>(g0) * rp;
   a.coef = e->plan_coef + gk * rp; a.rp = rp;
-  a.row_ptr_g0 = g0;
   const bool ready = e->last_plan_offsets && bitslice_rt8(e, stride);
   if (ready) a.joff = static_cast<const uint32_t*>(e->joff_dec) + gk * ((r + 7u) / 8u) * 16u;
   return launch_mac(e, true, a, st, "decode_mac launch", ready);
@@ -2667,14 +2665,14 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   if (rc) return rc;
   // the plan also writes the bit-sliced MAC's jump offsets when the apply will use them
   const bool offs = bitslice_rt8(e, stride);
-  if (G < kSplitMin || r == 0 || !split_batches(e, stride)) {
+  if (G < kSplitMin || r == 0 || !split_batches()) {
     rc = plan_impl(e, G, 0, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base,
                    status, stream, offs);
     if (rc) return rc;
     return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
   }
   if (!src || !rep) return fail(NTC_GPU_EINVAL, "NULL argument");
-  // plan A; then [MAC A on st | plan B, MAC B on side]; st joins the side stream
+  // plan A; [MAC A on st | plan B on side]; MAC B on st after both
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint32_t GA = G / 2, GB = G - GA;
   (void)hipSetDevice(e->device);
@@ -2686,9 +2684,9 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   if ((rc = plan_impl(e, G, GA, GB, k, r, src_len, src_mask, rep_size, rep_mask, sid_base,
                       rid_base, status, e->side, offs)))
     return rc;
-  if ((rc = apply_part(e, GA, GB, k, r, stride, src, rep, e->side))) return rc;
   if ((rc = apply_part(e, 0, GA, k, r, stride, src, rep, st))) return rc;
-  return join_side(e, st);
+  if ((rc = join_side(e, st))) return rc;
+  return apply_part(e, GA, GB, k, r, stride, src, rep, st);
 }
 
 uint32_t ntc_gf256_coef_pitch(uint32_t rows) { return tile_rp(rows); }

@@ -476,17 +476,14 @@ def cpu_baseline_dense(w, sample_bytes=1024):
 
 
 def kernel_summary(log, steps, dense):
-    """Per-step kernel times from a timing log of `steps` steps: {name: ms per step} and, per
-    step, the summed durations of the encode / decode MAC launches (batches of >= 512
-    generations run each MAC as two launches of G/2, overlapped with the other half's
-    preparation / plan)."""
+    """Per-step kernel times from the timing log of the timed steps: {name: ms per step} and the
+    per-launch durations of the encode / decode MAC kernels."""
     if not log or len(log) % steps:
         raise RuntimeError(f"timing log has {len(log)} entries for {steps} steps")
     per = len(log) // steps
     tot, launches = {}, {"encode_mac": [], "decode_mac": []}
     for s0 in range(0, len(log), per):
         seen_mac = seen_dense = 0
-        step = {"encode_mac": 0.0, "decode_mac": 0.0}
         for name, ms in log[s0:s0 + per]:
             if dense and name == "encode_mac":       # dense step: encode combine, decode combine
                 name = "decode_mac" if seen_mac else "encode_mac"
@@ -495,10 +492,8 @@ def kernel_summary(log, steps, dense):
                 name = "dense_invert" if seen_dense else "dense_encode_layout"
                 seen_dense += 1
             tot[name] = tot.get(name, 0.0) + ms
-            if name in step:
-                step[name] += ms
-        for name in launches:
-            launches[name].append(step[name])
+            if name in launches:
+                launches[name].append(ms)
     return {n: v / steps for n, v in tot.items()}, launches
 
 
@@ -626,11 +621,9 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": tsrc, "kernel": dom, "kernel_ms": round(t_dom, 4),
-            "kernel_ms_source": f"{dom} time per timed step, mean over the {len(launches[dom])} "
-                                f"timed steps (HIP event pairs on the launch stream around each "
-                                f"launch; a batch of G >= 512 runs as two launches of G/2, summed)",
+            "kernel_ms_source": f"mean of the {len(launches[dom])} {dom} launches of the timed "
+                                f"steps (HIP event pairs on the launch stream)",
             "algorithmic_bytes_per_launch": int(bytes_dom),
-            "algorithmic_bytes_note": "per step's MAC (both halves): the whole batch's bytes",
             "byte_macs_per_launch": int(macs),
             "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2),
             "valu_profile": valu, "valu_profile_source": vsrc,

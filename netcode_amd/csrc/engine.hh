@@ -37,11 +37,6 @@ struct ntc_gf256_engine {
   uint32_t tlog_mask = ~0u;            // bit k: log kernels of kind k (ntc_gf256_timing_kinds)
   std::vector<hipEvent_t> tlog_ev;     // 2 per entry
   std::vector<uint32_t> tlog_kind;     // NTC_GF256_K_*
-  // split batches (encode / decode of G >= kSplitMin generations run as two halves): the second
-  // half's preparation / plan runs on `side` while the first half's MAC runs on the caller's
-  // stream; ev_side[0] forks, ev_side[1] joins
-  hipStream_t side = nullptr;
-  hipEvent_t ev_side[2] = {nullptr, nullptr};
   // geometry of the last plan (decode_apply must match)
   uint32_t last_G = 0, last_k = 0, last_r = 0, last_rp = 0;
   // dense-code workspace (ntc_dense.hip): augmented matrices (ping-pong), panel trackers,

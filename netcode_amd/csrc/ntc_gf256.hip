@@ -827,7 +827,6 @@ __device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
 
 struct PrepArgs {
   uint32_t G, k, r, rp;
-  uint32_t g0;         // first generation of this launch in the caller's batch (default ids)
   const uint16_t* src_len;
   const uint32_t* sid_base;
   const uint32_t* rid_base;
@@ -841,8 +840,8 @@ struct PrepArgs {
 __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
 {
   const uint32_t g = blockIdx.x;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : (a.g0 + g) * a.k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : (a.g0 + g) * a.r;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
   // LDS copies of the v_perm tables (encoded sizes) and of the block offsets (jump offsets):
   // per-lane lookups that would otherwise be dependent global loads
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
@@ -925,7 +924,6 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
 // singularity (rank) is pivot-order independent too.
 struct PlanArgs {
   uint32_t G, k, r;
-  uint32_t g0;       // first generation of this launch in the caller's batch (default ids)
   uint16_t* src_len;
   const uint8_t* src_mask;
   const uint16_t* rep_size;
@@ -1028,8 +1026,8 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
 
 
   const uint32_t k = a.k, r = a.r;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : (a.g0 + g) * k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : (a.g0 + g) * r;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
   const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
   const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -1342,8 +1340,8 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t g = blockIdx.x;
   const uint32_t k = a.k, r = a.r;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : (a.g0 + g) * k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : (a.g0 + g) * r;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
   const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
   const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -1728,8 +1726,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   };
 
   const uint32_t k = a.k, r = a.r;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : (a.g0 + g) * k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : (a.g0 + g) * r;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
   const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
   const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -2276,9 +2274,6 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
       if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : e->tlog_ev)
     if (ev) (void)hipEventDestroy(ev);
-  for (hipEvent_t ev : e->ev_side)
-    if (ev) (void)hipEventDestroy(ev);
-  if (e->side) (void)hipStreamDestroy(e->side);
   delete e;
 }
 
@@ -2379,105 +2374,6 @@ int ntc_gf256_reserve(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r)
   return ensure_plan(e, G, k, rp);
 }
 
-// Encode of generations [g0, g0 + Gh) of a batch: preparation then MAC, or only one of them.
-static int encode_part(ntc_gf256_engine* e, uint32_t g0, uint32_t Gh, uint32_t k, uint32_t r,
-                       uint32_t stride, const uint8_t* src, const uint16_t* src_len,
-                       const uint32_t* sid_base, const uint32_t* rid_base, uint8_t* rep,
-                       uint16_t* rep_size, uint16_t* rep_len, hipStream_t st, bool fused,
-                       bool prep, bool mac)
-{
-  const uint32_t rp = tile_rp(r);
-  const uint32_t ntiles = (r + 7u) / 8u;
-  int rc;
-  if (prep) {
-    PrepArgs p{};
-    p.G = Gh; p.k = k; p.r = r; p.rp = rp; p.g0 = g0;
-    p.src_len = src_len + static_cast<size_t>(g0) * k;
-    p.sid_base = sid_base ? sid_base + g0 : nullptr;
-    p.rid_base = rid_base ? rid_base + g0 : nullptr;
-    p.rep_size = rep_size + static_cast<size_t>(g0) * r;
-    p.rep_len = rep_len ? rep_len + g0 : nullptr;
-    if (fused) {
-      p.ntiles = ntiles;
-      p.joff = static_cast<uint32_t*>(e->joff) + static_cast<size_t>(g0) * k * ntiles * 16u;
-    } else {
-      p.coef = static_cast<uint8_t*>(e->enc_coef) + static_cast<size_t>(g0) * k * rp;
-    }
-    {
-      KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st);
-      hipLaunchKernelGGL(encode_prep, dim3(Gh), dim3(256), 0, st, p);
-    }
-    if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
-  }
-  if (!mac) return NTC_GPU_OK;
-  MacArgs a{};
-  a.G = Gh; a.k = k; a.rows = r; a.stride = stride;
-  a.in0 = src + static_cast<size_t>(g0) * k * stride;
-  a.out = rep + static_cast<size_t>(g0) * r * stride;
-  a.coef = static_cast<const uint8_t*>(e->enc_coef) + static_cast<size_t>(g0) * k * rp;
-  a.rp = rp;
-  if (e->joff) a.joff = static_cast<const uint32_t*>(e->joff) + (fused ? static_cast<size_t>(g0) * k * ntiles * 16u : 0u);
-  return launch_mac(e, false, a, st, "encode_mac launch", fused);
-}
-
-// Batches of at least kSplitMin generations run as two halves so that the second half's
-// latency-bound preparation / plan kernel overlaps the first half's VALU-bound MAC (on the
-// engine's side stream); NTC_GF256_SPLIT=0 turns this off (A/B runs).
-constexpr uint32_t kSplitMin = 512;
-
-static bool split_batches()
-{
-  static const bool on = [] {
-    const char* v = std::getenv("NTC_GF256_SPLIT");
-    return !(v && std::atoi(v) == 0);
-  }();
-  return on;
-}
-
-static int ensure_side(ntc_gf256_engine* e)
-{
-  if (e->side) return NTC_GPU_OK;
-  int rc;
-  for (hipEvent_t& ev : e->ev_side)
-    if (!ev && (rc = hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate")))
-      return rc;
-  return hip_check(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking), "hipStreamCreate side");
-}
-
-// Size the workspace launch_mac allocates for a batch of G generations up front, so the launches
-// of a split batch never reallocate a buffer an earlier half's kernel may still be using.
-static int presize_mac(ntc_gf256_engine* e, bool dec, uint32_t G, uint32_t k, uint32_t rows,
-                       uint32_t stride)
-{
-  if (!use_bitslice(e, stride)) return NTC_GPU_OK;
-  int rc;
-  if (dec && (rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap,
-                              static_cast<uint64_t>(G) * (k + kBjRing) * 8, "hipMalloc row_ptr")))
-    return rc;
-  const int gv = gx_chain();
-  if (gv >= 2) return NTC_GPU_OK;                     // coefficient bytes read directly
-  // gx 1: 16 B per (generation, source, 8-row tile); nibble chain: 2 * rt u32 per (.., rt-row tile)
-  const size_t n = static_cast<size_t>(G) * k * ((rows + 7u) / 8u + 1u) * 64u;
-  return ensure_buf(&e->joff, &e->joff_cap, n, "hipMalloc joff");
-}
-
-// side stream waits for everything queued on st so far
-static int fork_side(ntc_gf256_engine* e, hipStream_t st)
-{
-  int rc = ensure_side(e);
-  if (rc) return rc;
-  if ((rc = hip_check(hipEventRecord(e->ev_side[0], st), "hipEventRecord fork"))) return rc;
-  return hip_check(hipStreamWaitEvent(e->side, e->ev_side[0], 0), "hipStreamWaitEvent fork");
-}
-
-// st waits for everything queued on the side stream so far
-static int join_side(ntc_gf256_engine* e, hipStream_t st)
-{
-  int rc = hip_check(hipEventRecord(e->ev_side[1], e->side), "hipEventRecord join");
-  if (rc) return rc;
-  return hip_check(hipStreamWaitEvent(st, e->ev_side[1], 0), "hipStreamWaitEvent join");
-}
-
 int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
                            uint32_t stride, const uint8_t* src, const uint16_t* src_len,
                            const uint32_t* sid_base, const uint32_t* rid_base, uint8_t* rep,
@@ -2490,6 +2386,9 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   (void)hipSetDevice(e->device);
   const uint32_t rp = tile_rp(r);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  PrepArgs p{};
+  p.G = G; p.k = k; p.r = r; p.rp = rp; p.src_len = src_len; p.sid_base = sid_base;
+  p.rid_base = rid_base; p.rep_size = rep_size; p.rep_len = rep_len;
   // bit-sliced MAC with 8-row tiles: the preparation writes the jump offsets directly
   static const bool rows16 = [] {
     const char* v = std::getenv("NTC_GF256_BJ_ROWS");
@@ -2497,39 +2396,32 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   }();
   const bool fused = use_bitslice(e, stride) && !rows16 && !gx_chain();
   if (fused) {
-    const size_t n = static_cast<size_t>(G) * k * ((r + 7u) / 8u) * 16u;
+    p.ntiles = (r + 7u) / 8u;
+    const size_t n = static_cast<size_t>(G) * k * p.ntiles * 16u;
     rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
+    if (rc) return rc;
+    p.joff = static_cast<uint32_t*>(e->joff);
   } else {
     rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+    if (rc) return rc;
+    p.coef = static_cast<uint8_t*>(e->enc_coef);
   }
-  if (rc) return rc;
-  if (G < kSplitMin || !split_batches())
-    return encode_part(e, 0, G, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
-                       rep_len, st, fused, true, true);
-  // prep A; [MAC A on st | prep B on side]; MAC B on st after both
-  const uint32_t GA = G / 2, GB = G - GA;
-  if ((rc = presize_mac(e, false, G, k, r, stride))) return rc;
-  if ((rc = encode_part(e, 0, GA, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
-                        rep_len, st, fused, true, false)))
-    return rc;
-  if ((rc = fork_side(e, st))) return rc;
-  if ((rc = encode_part(e, GA, GB, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
-                        rep_len, e->side, fused, true, false)))
-    return rc;
-  if ((rc = encode_part(e, 0, GA, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
-                        rep_len, st, fused, false, true)))
-    return rc;
-  if ((rc = join_side(e, st))) return rc;
-  return encode_part(e, GA, GB, k, r, stride, src, src_len, sid_base, rid_base, rep, rep_size,
-                     rep_len, st, fused, false, true);
+  {
+    KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st);
+    hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
+  }
+  if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
+  MacArgs a{};
+  a.G = G; a.k = k; a.rows = r; a.stride = stride;
+  a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
+  a.joff = static_cast<const uint32_t*>(e->joff);
+  return launch_mac(e, false, a, st, "encode_mac launch", fused);
 }
 
-// Plan of generations [g0, g0 + G) of a batch of Gall generations (pointers are the batch's).
-static int plan_impl(ntc_gf256_engine* e, uint32_t Gall, uint32_t g0, uint32_t G, uint32_t k,
-                     uint32_t r, uint16_t* src_len, const uint8_t* src_mask,
-                     const uint16_t* rep_size, const uint8_t* rep_mask, const uint32_t* sid_base,
-                     const uint32_t* rid_base, ntc_gf256_decode_status* status, void* stream,
-                     bool offsets)
+static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, uint16_t* src_len,
+                     const uint8_t* src_mask, const uint16_t* rep_size, const uint8_t* rep_mask,
+                     const uint32_t* sid_base, const uint32_t* rid_base,
+                     ntc_gf256_decode_status* status, void* stream, bool offsets)
 {
   if (!e || !src_len || !src_mask || !rep_size || !rep_mask || !status)
     return fail(NTC_GPU_EINVAL, "NULL argument");
@@ -2549,24 +2441,19 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t Gall, uint32_t g0, uint32_t G
   if (k > 65535) return fail(NTC_GPU_EUNSUPPORTED, "k > 65535");
   const uint32_t rp = tile_rp(r);
   (void)hipSetDevice(e->device);
-  int rc = ensure_plan(e, Gall, k, rp);
+  int rc = ensure_plan(e, G, k, rp);
   if (rc) return rc;
-  const size_t gk = static_cast<size_t>(g0) * k, gr = static_cast<size_t>(g0) * r;
   PlanArgs p{};
-  p.G = G; p.k = k; p.r = r; p.g0 = g0;
-  p.src_len = src_len + gk; p.src_mask = src_mask + gk; p.rep_size = rep_size + gr;
-  p.rep_mask = rep_mask + gr;
-  p.sid_base = sid_base ? sid_base + g0 : nullptr;
-  p.rid_base = rid_base ? rid_base + g0 : nullptr;
-  p.status = status + g0;
-  p.plan_m = e->plan_m + g0; p.plan_in = e->plan_in + gk; p.plan_out = e->plan_out + static_cast<size_t>(g0) * rp;
-  p.plan_coef = e->plan_coef + gk * rp; p.rp = rp;
+  p.G = G; p.k = k; p.r = r; p.src_len = src_len; p.src_mask = src_mask; p.rep_size = rep_size;
+  p.rep_mask = rep_mask; p.sid_base = sid_base; p.rid_base = rid_base; p.status = status;
+  p.plan_m = e->plan_m; p.plan_in = e->plan_in; p.plan_out = e->plan_out;
+  p.plan_coef = e->plan_coef; p.rp = rp;
   if (offsets && r > 0) {
     p.ntiles = (r + 7u) / 8u;
-    rc = ensure_buf(&e->joff_dec, &e->joff_dec_cap, static_cast<size_t>(Gall) * k * p.ntiles * 64u,
+    rc = ensure_buf(&e->joff_dec, &e->joff_dec_cap, static_cast<size_t>(G) * k * p.ntiles * 64u,
                     "hipMalloc joff_dec");
     if (rc) return rc;
-    p.joff = static_cast<uint32_t*>(e->joff_dec) + gk * p.ntiles * 16u;
+    p.joff = static_cast<uint32_t*>(e->joff_dec);
   }
   static const uint32_t ablate = [] {
     const char* v = std::getenv("NTC_GF256_PLAN_ABLATE");
@@ -2602,7 +2489,7 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t Gall, uint32_t g0, uint32_t G
     auto* fn = r <= 8 ? decode_plan<8> : r <= 16 ? decode_plan<16> : r <= 32 ? decode_plan<32> : decode_plan<64>;
     hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
   }
-  e->last_G = Gall; e->last_k = k; e->last_r = r; e->last_rp = rp;
+  e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
   e->last_plan_offsets = p.joff != nullptr;
   return hip_check(hipGetLastError(), "decode_plan launch");
 }
@@ -2622,25 +2509,8 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
                           const uint8_t* rep_mask, const uint32_t* sid_base,
                           const uint32_t* rid_base, ntc_gf256_decode_status* status, void* stream)
 {
-  return plan_impl(e, G, 0, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base,
-                   status, stream, false);
-}
-
-// Region MAC of the plan of generations [g0, g0 + G) (the engine's plan arrays hold the batch).
-static int apply_part(ntc_gf256_engine* e, uint32_t g0, uint32_t G, uint32_t k, uint32_t r,
-                      uint32_t stride, uint8_t* src, const uint8_t* rep, hipStream_t st)
-{
-  const uint32_t rp = e->last_rp;
-  const size_t gk = static_cast<size_t>(g0) * k;
-  MacArgs a{};
-  a.G = G; a.k = k; a.rows = r; a.stride = stride;
-  a.out = src + gk * stride; a.in0 = a.out; a.in1 = rep + static_cast<size_t>(g0) * r * stride;
-  a.rows_per_gen = e->plan_m + g0; a.in_idx = e->plan_in + gk;
-  a.out_idx = e->plan_out + static_cast<size_t>(g0) * rp;
-  a.coef = e->plan_coef + gk * rp; a.rp = rp;
-  const bool ready = e->last_plan_offsets && bitslice_rt8(e, stride);
-  if (ready) a.joff = static_cast<const uint32_t*>(e->joff_dec) + gk * ((r + 7u) / 8u) * 16u;
-  return launch_mac(e, true, a, st, "decode_mac launch", ready);
+  return plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
+                   stream, false);
 }
 
 int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -2652,7 +2522,14 @@ int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   if (G != e->last_G || k != e->last_k || r != e->last_r)
     return fail(NTC_GPU_EINVAL, "decode_apply geometry differs from the last decode_plan");
   if (r == 0) return NTC_GPU_OK;
-  return apply_part(e, 0, G, k, r, stride, src, rep, static_cast<hipStream_t>(stream));
+  MacArgs a{};
+  a.G = G; a.k = k; a.rows = r; a.stride = stride;
+  a.in0 = src; a.in1 = rep; a.out = src;
+  a.rows_per_gen = e->plan_m; a.in_idx = e->plan_in; a.out_idx = e->plan_out;
+  a.coef = e->plan_coef; a.rp = e->last_rp;
+  const bool ready = e->last_plan_offsets && bitslice_rt8(e, stride);
+  if (ready) a.joff = static_cast<const uint32_t*>(e->joff_dec);
+  return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch", ready);
 }
 
 int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -2664,29 +2541,10 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   int rc = check_shape(G, k, r, stride);
   if (rc) return rc;
   // the plan also writes the bit-sliced MAC's jump offsets when the apply will use them
-  const bool offs = bitslice_rt8(e, stride);
-  if (G < kSplitMin || r == 0 || !split_batches()) {
-    rc = plan_impl(e, G, 0, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base,
-                   status, stream, offs);
-    if (rc) return rc;
-    return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
-  }
-  if (!src || !rep) return fail(NTC_GPU_EINVAL, "NULL argument");
-  // plan A; [MAC A on st | plan B on side]; MAC B on st after both
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const uint32_t GA = G / 2, GB = G - GA;
-  (void)hipSetDevice(e->device);
-  if ((rc = presize_mac(e, true, G, k, r, stride))) return rc;
-  if ((rc = plan_impl(e, G, 0, GA, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base,
-                      status, st, offs)))
-    return rc;
-  if ((rc = fork_side(e, st))) return rc;
-  if ((rc = plan_impl(e, G, GA, GB, k, r, src_len, src_mask, rep_size, rep_mask, sid_base,
-                      rid_base, status, e->side, offs)))
-    return rc;
-  if ((rc = apply_part(e, 0, GA, k, r, stride, src, rep, st))) return rc;
-  if ((rc = join_side(e, st))) return rc;
-  return apply_part(e, GA, GB, k, r, stride, src, rep, st);
+  rc = plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
+                 stream, bitslice_rt8(e, stride));
+  if (rc) return rc;
+  return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
 }
 
 uint32_t ntc_gf256_coef_pitch(uint32_t rows) { return tile_rp(rows); }

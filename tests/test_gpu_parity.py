@@ -289,30 +289,3 @@ def test_mac_timing_api(gpu):
         assert ms.value > 0
     finally:
         _native.check(L.ntc_gf256_set_timing(h, 0), "timing")
-
-
-@pytest.mark.parametrize("G,k,r,S,explicit", [(513, 16, 4, 256, False), (600, 24, 12, 2048, True),
-                                               (1025, 40, 40, 64, False)])
-def test_split_batches(gpu, mac, oracle, G, k, r, S, explicit):
-    """Batches of >= 512 generations run encode and decode as two halves (the second half's
-    preparation / plan on the engine's side stream, overlapping the first half's MAC): same
-    bytes, sizes and status as the oracle over the whole batch, with default ids (g*k / g*r of
-    the whole batch, not of the half) and explicit ones; r = 40 covers the LDS plan's screening."""
-    seed = G + k
-    src, lens = make_sources(G, k, S, S, seed=seed, ragged=True)
-    sid = (np.arange(G) * (k + 5) + 11).astype(np.uint32) if explicit else None
-    rid = (np.arange(G) * (r + 3) + 7).astype(np.uint32) if explicit else None
-    rep, rsz, _ = gpu_encode(gpu, src, lens, k, r, sid, rid)
-    orep, orsz = oracle.encode_batch(src, lens, k, r, sid, rid)
-    assert (rep == orep).all() and (rsz == orsz).all()
-    smask = loss_iid((G, k), 0.3, seed + 1)
-    rmask = loss_iid((G, r), 0.2, seed + 2)
-    lost = src.copy()
-    lost[smask == 0] = 0
-    llen = lens.copy()
-    llen[smask == 0] = 0
-    out, olen, st = gpu_decode(gpu, lost, llen, smask, rep, rsz, rmask, sid, rid)
-    oout, oolen, ost = oracle.decode_batch(lost, llen, smask, orep, orsz, rmask, sid, rid)
-    assert (st == ost).all()
-    assert (olen == oolen).all()
-    assert (out == oout).all()

@@ -940,6 +940,8 @@ struct PlanArgs {
   uint32_t* joff;    // non-null: also write the bit-sliced MAC's jump offsets (8-row tiles)
   uint32_t ntiles;
   uint32_t big_rows, big_pitch;   // decode_plan_big: LDS matrix shape
+  uint32_t m_cap;                 // decode_plan_big: > 0: defer generations with m > m_cap
+  uint32_t deferred_only;         // decode_plan_big: only the generations an m_cap pass deferred
 };
 
 // Jump offsets of one (input position, 8-row tile, 2-row quad) from the two rows' coefficients
@@ -1314,12 +1316,18 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
 // Windows this large are rare, so this kernel favours simplicity over speed (block barriers per
 // pivot), but every step stays on the device.
 constexpr uint32_t kBigRows = 255;
+// decode_plan_big sizes its LDS matrix for m <= kBigCap first (several workgroups per CU); the
+// generations with more missing sources are marked with this state and planned by a second,
+// full-size launch that skips every other generation
+constexpr uint32_t kBigCap = 64;
+constexpr uint8_t kPlanDeferred = 0x80;
 
 __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t big_lds[];
   // A: a.big_rows rows (>= r) of a.big_pitch dwords (>= 2r bytes, odd: conflict-free per row),
   // sized per launch so small windows fit several workgroups per CU
+  if (a.deferred_only && a.status[blockIdx.x].state != kPlanDeferred) return;   // uniform
   const uint32_t P = a.big_pitch;
   uint32_t* A = big_lds;
   uint16_t* miss = reinterpret_cast<uint16_t*>(big_lds + a.big_rows * P);  // [256]
@@ -1381,6 +1389,8 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
     st.nb_useless = static_cast<uint16_t>(nrecv);
   } else if (nrecv < m || m > kBigRows) {
     st.state = 2;
+  } else if (a.m_cap && m > a.m_cap) {
+    st.state = kPlanDeferred;                 // this launch's matrix rows are too short
   } else {
     const uint32_t nw = (2 * m + 3) / 4;
     auto byte_at = [&](uint32_t row, uint32_t c) -> uint32_t {
@@ -1597,9 +1607,10 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
 }
 // dynamic LDS of decode_plan_big: matrix + miss/recv/reps/rl (u16) + szs + counters + v_perm tables
 // (big_rows * big_pitch is padded to a multiple of 4 dwords, so ptab stays 16-byte aligned)
-inline size_t big_lds_bytes(uint32_t rows, uint32_t pitch)
+inline size_t big_lds_bytes(uint32_t rows, uint32_t pitch, uint32_t mmax)
 {
-  return (static_cast<size_t>(rows) * pitch + 5 * 128 + 256 + 8 + 256 * 8 + 256 * 8) * 4;
+  // A, miss/recv/reps/rl/sl (5 x 256 u16), szs, wcnt, v_perm tables, c4 [mmax][8]
+  return (static_cast<size_t>(rows) * pitch + 5 * 128 + 256 + 8 + 256 * 8 + mmax * 8) * 4;
 }
 
 // ------------------------------------------------------------- decode plan, r <= 32 (v2) ----
@@ -2469,17 +2480,28 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
   }();
   KernelTimer kt(e, NTC_GF256_K_DECODE_PLAN, static_cast<hipStream_t>(stream));
   if (big) {
-    p.big_pitch = ((2 * r + 3) / 4) | 1u;
-    p.big_rows = r;
-    while ((p.big_rows * p.big_pitch) % 4u) ++p.big_rows;
     static const int lds_ok = [] {
       return static_cast<int>(hipFuncSetAttribute(reinterpret_cast<const void*>(decode_plan_big),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  static_cast<int>(big_lds_bytes(260, 129))));
+                                                  static_cast<int>(big_lds_bytes(260, 129, 256))));
     }();
     if (lds_ok != 0) return fail(NTC_GPU_EDEVICE, "decode_plan_big: LDS attribute");
-    hipLaunchKernelGGL(decode_plan_big, dim3(G), dim3(256), big_lds_bytes(p.big_rows, p.big_pitch),
-                       static_cast<hipStream_t>(stream), p);
+    // matrix rows of 2 * mmax bytes (odd dword pitch), r rows padded so ptab stays 16-B aligned
+    auto launch_big = [&](uint32_t mmax, uint32_t cap, uint32_t deferred) {
+      p.big_pitch = ((2 * mmax + 3) / 4) | 1u;
+      p.big_rows = r;
+      while ((p.big_rows * p.big_pitch) % 4u) ++p.big_rows;
+      p.m_cap = cap;
+      p.deferred_only = deferred;
+      hipLaunchKernelGGL(decode_plan_big, dim3(G), dim3(256), big_lds_bytes(p.big_rows, p.big_pitch, mmax),
+                         static_cast<hipStream_t>(stream), p);
+    };
+    if (r > kBigCap) {
+      launch_big(kBigCap, kBigCap, 0);          // every generation with m <= kBigCap
+      launch_big(r, 0, 1);                      // the deferred ones, full-size rows
+    } else {
+      launch_big(r, 0, 0);
+    }
   } else if (r <= 32 && !lds_plan && !ablate) {
     p.ablate = ablate_w;
     auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;

@@ -1404,7 +1404,9 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
     // received rows (pivots chosen among the first m-1 only) leaves every candidate row reduced
     // against that basis; the first nonzero one is the repair that completes decoding.
     bool found = false;
-    {
+    if (a.ablate & 16u) {        // timing ablation: no screening (results wrong)
+      found = true;
+    } else {
       const uint32_t nwl = (m + 3) / 4;
       if (tid < nrecv) {   // row i: received repair i over the missing sources
         const uint32_t rid = ridb + recv[tid];
@@ -1479,7 +1481,7 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
       }
       __syncthreads();
       bool singular = false;
-      for (uint32_t p = 0; p < m; ++p) {
+      for (uint32_t p = 0; p < m && !(a.ablate & 32u); ++p) {   // bit 32: timing ablation
         if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
         __syncthreads();
         if (tid >= p && tid < m && byte_at(tid, p) != 0) atomicMin(&wcnt[4], tid);
@@ -1547,11 +1549,11 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
           sl[i] = slen[rl[i]];
         }
         __syncthreads();
-        if (tid < m)
+        if (tid < m && !(a.ablate & 128u))     // bit 128: timing ablation
           for (uint32_t i = 0; i < cnt; ++i) red ^= mul4(ptab[coefficient(rid_t, sidb + rl[i])], sl[i]);
         // 32 positions at a time: thread s takes the table of (M^-1)[s][q] once per q and
         // multiplies four positions' coefficients c(q, j..j+3) per mul4
-        for (uint32_t i0 = 0; i0 < cnt; i0 += 32) {
+        for (uint32_t i0 = 0; i0 < ((a.ablate & 64u) ? 0u : cnt); i0 += 32) {   // bit 64: ablation
           const uint32_t n32 = min(32u, cnt - i0);
           __syncthreads();                      // the previous block's c4 reads are done
           for (uint32_t e = tid; e < m * 8u; e += 256) {

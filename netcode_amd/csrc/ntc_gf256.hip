@@ -1396,17 +1396,65 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
     auto byte_at = [&](uint32_t row, uint32_t c) -> uint32_t {
       return (A[(row) * P + (c >> 2)] >> (8 * (c & 3))) & 0xFFu;
     };
-    bool ok = false;
+    // Gauss-Jordan on {first m-1 received repairs} + {received repair t} -> [I | M^-1] in rows
+    // 0..m-1 of A; false when singular (decoder.cc:448-468 drops repair t)
+    auto attempt = [&](uint32_t t) -> bool {
+      if (tid < m) {       // thread q builds row q: coefficients of the missing sources | identity
+        const uint32_t rq = (tid + 1 < m) ? recv[tid] : recv[t];
+        reps[tid] = static_cast<uint16_t>(rq);
+        const uint32_t rid = ridb + rq;
+        for (uint32_t w = 0; w < nw; ++w) {
+          uint32_t word = 0;
+          for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t c = 4 * w + b;
+            uint32_t v = 0;
+            if (c < m) v = coefficient(rid, sidb + miss[c]);
+            else if (c < 2 * m) v = (c - m == tid) ? 1u : 0u;
+            word |= v << (8 * b);
+          }
+          A[(tid) * P + (w)] = word;
+        }
+      }
+      __syncthreads();
+      for (uint32_t p = 0; p < m && !(a.ablate & 32u); ++p) {   // bit 32: timing ablation
+        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid >= p && tid < m && byte_at(tid, p) != 0) atomicMin(&wcnt[4], tid);
+        __syncthreads();
+        const uint32_t q = wcnt[4];
+        if (q == 0xFFFFFFFFu) return false;           // uniform
+        if (q != p) {
+          for (uint32_t w = tid; w < nw; w += 256) {
+            const uint32_t tmp = A[(p) * P + (w)];
+            A[(p) * P + (w)] = A[(q) * P + (w)];
+            A[(q) * P + (w)] = tmp;
+          }
+          __syncthreads();
+        }
+        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(p, p))];
+        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
+        for (uint32_t w = tid; w < nw; w += 256) A[(p) * P + (w)] = mul4(tinv, A[(p) * P + (w)]);
+        __syncthreads();
+        const uint32_t fa = (tid < m && tid != p) ? byte_at(tid, p) : 0u;
+        if (fa != 0) {
+          const uint32_t* tf0 = ptab[fa];
+          const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
+          for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(p) * P + (w)]);
+        }
+        __syncthreads();
+      }
+      return true;
+    };
     uint32_t t = m - 1;
-    // Screening (same outcome as trying t = m-1, m, ... with a full Gauss-Jordan each, as
-    // decoder.cc:448-468 does): {first m-1 repairs} + {t} is invertible iff the first m-1 rows
-    // are independent and row t is outside their span.  One forward elimination over all
-    // received rows (pivots chosen among the first m-1 only) leaves every candidate row reduced
-    // against that basis; the first nonzero one is the repair that completes decoding.
-    bool found = false;
-    if (a.ablate & 16u) {        // timing ablation: no screening (results wrong)
-      found = true;
-    } else {
+    bool ok = attempt(t);
+    if (!ok && t + 1 < nrecv && !(a.ablate & 16u)) {   // bit 16: timing ablation
+      // Screening (same outcome as trying t = m, m+1, ... with a full Gauss-Jordan each, as
+      // decoder.cc:448-468 does): {first m-1 repairs} + {t} is invertible iff the first m-1 rows
+      // are independent and row t is outside their span.  One forward elimination over all
+      // received rows (pivots chosen among the first m-1 only) leaves every candidate row
+      // reduced against that basis; the first nonzero one is the repair that completes
+      // decoding (none: every candidate fails).
+      __syncthreads();
       const uint32_t nwl = (m + 3) / 4;
       if (tid < nrecv) {   // row i: received repair i over the missing sources
         const uint32_t rid = ridb + recv[tid];
@@ -1441,11 +1489,15 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         for (uint32_t w = tid; w < nwl; w += 256) A[(rank) * P + (w)] = mul4(tinv, A[(rank) * P + (w)]);
         __syncthreads();
         const uint32_t fa = (tid > rank && tid < nrecv) ? byte_at(tid, c) : 0u;
-        if (fa != 0)
-          for (uint32_t w = 0; w < nwl; ++w) A[(tid) * P + (w)] ^= mul4(ptab[fa], A[(rank) * P + (w)]);
+        if (fa != 0) {
+          const uint32_t* tf0 = ptab[fa];
+          const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
+          for (uint32_t w = 0; w < nwl; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(rank) * P + (w)]);
+        }
         __syncthreads();
         ++rank;
       }
+      uint32_t next = nrecv;
       if (rank + 1 == m) {
         if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
         __syncthreads();
@@ -1455,61 +1507,13 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
           if (nz != 0) atomicMin(&wcnt[4], tid);
         }
         __syncthreads();
-        if (wcnt[4] != 0xFFFFFFFFu) {
-          found = true;
-          t = wcnt[4];
-        }
+        next = wcnt[4] != 0xFFFFFFFFu ? wcnt[4] : nrecv;
       }
       __syncthreads();
-    }
-    for (; found && t < nrecv; ++t) {   // one iteration: M^-1 for the chosen candidate
-      if (tid < m) {       // thread q builds row q: coefficients of the missing sources | identity
-        const uint32_t rq = (tid + 1 < m) ? recv[tid] : recv[t];
-        reps[tid] = static_cast<uint16_t>(rq);
-        const uint32_t rid = ridb + rq;
-        for (uint32_t w = 0; w < nw; ++w) {
-          uint32_t word = 0;
-          for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t c = 4 * w + b;
-            uint32_t v = 0;
-            if (c < m) v = coefficient(rid, sidb + miss[c]);
-            else if (c < 2 * m) v = (c - m == tid) ? 1u : 0u;
-            word |= v << (8 * b);
-          }
-          A[(tid) * P + (w)] = word;
-        }
+      if (next < nrecv) {
+        t = next;
+        ok = attempt(t);                              // invertible by construction
       }
-      __syncthreads();
-      bool singular = false;
-      for (uint32_t p = 0; p < m && !(a.ablate & 32u); ++p) {   // bit 32: timing ablation
-        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
-        __syncthreads();
-        if (tid >= p && tid < m && byte_at(tid, p) != 0) atomicMin(&wcnt[4], tid);
-        __syncthreads();
-        const uint32_t q = wcnt[4];
-        if (q == 0xFFFFFFFFu) { singular = true; break; }
-        if (q != p) {
-          for (uint32_t w = tid; w < nw; w += 256) {
-            const uint32_t tmp = A[(p) * P + (w)];
-            A[(p) * P + (w)] = A[(q) * P + (w)];
-            A[(q) * P + (w)] = tmp;
-          }
-          __syncthreads();
-        }
-        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(p, p))];
-        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
-        for (uint32_t w = tid; w < nw; w += 256) A[(p) * P + (w)] = mul4(tinv, A[(p) * P + (w)]);
-        __syncthreads();
-        const uint32_t fa = (tid < m && tid != p) ? byte_at(tid, p) : 0u;
-        if (fa != 0) {
-          const uint32_t* tf0 = ptab[fa];
-          const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
-          for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(p) * P + (w)]);
-        }
-        __syncthreads();
-      }
-      ok = !singular;
-      break;
     }
     if (!ok) {
       st.state = 3;

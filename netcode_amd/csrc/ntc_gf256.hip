@@ -1335,9 +1335,11 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
   uint16_t* reps = recv + 256;                                             // [256]
   uint16_t* rl = reps + 256;                                               // [256] chunk list
   uint16_t* sl = rl + 256;                                                 // [256] its lengths
-  uint32_t* szs = reinterpret_cast<uint32_t*>(sl + 256);                   // [256]
+  uint16_t* pivrow = sl + 256;                                             // [256] row of pivot col
+  uint32_t* szs = reinterpret_cast<uint32_t*>(pivrow + 256);               // [256]
   uint32_t* wcnt = szs + 256;                                              // [4] + [1] (+3)
-  uint32_t (*ptab)[8] = reinterpret_cast<uint32_t (*)[8]>(wcnt + 8);       // v_perm tables, 8 KiB
+  uint32_t* wmin = wcnt + 8;                                               // [2][4] pivot votes
+  uint32_t (*ptab)[8] = reinterpret_cast<uint32_t (*)[8]>(wcnt + 16);      // v_perm tables, 8 KiB
   uint32_t* c4 = &ptab[0][0] + 256 * 8;       // [m][8]: c(q, j) of 32 received positions, packed
   {   // per-thread coefficients index the tables divergently: serve them from LDS
     const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
@@ -1396,8 +1398,20 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
     auto byte_at = [&](uint32_t row, uint32_t c) -> uint32_t {
       return (A[(row) * P + (c >> 2)] >> (8 * (c & 3))) & 0xFFu;
     };
-    // Gauss-Jordan on {first m-1 received repairs} + {received repair t} -> [I | M^-1] in rows
-    // 0..m-1 of A; false when singular (decoder.cc:448-468 drops repair t)
+    // Lowest row index voted by the block: each wave posts its lowest `hit` lane to wmin[par][wv]
+    // (double-buffered by `par`, so a wave racing ahead to the next vote cannot overwrite a slot
+    // still being read), one barrier, every thread takes the minimum.  0xFFFFFFFF: no vote.
+    auto vote = [&](bool hit, uint32_t par) -> uint32_t {
+      const uint64_t b = __ballot(hit);
+      if (lane == 0) wmin[par * 4 + wv] = b ? wv * 64u + (__ffsll(static_cast<long long>(b)) - 1) : 0xFFFFFFFFu;
+      __syncthreads();
+      return min(min(wmin[par * 4], wmin[par * 4 + 1]), min(wmin[par * 4 + 2], wmin[par * 4 + 3]));
+    };
+    // Gauss-Jordan on {first m-1 received repairs} + {received repair t} (decoder.cc:448-468
+    // drops repair t when singular).  No row swaps and no per-pivot normalisation: the pivot of
+    // column p is the lowest not-yet-pivot row with a nonzero there (pivrow[p]); every other row
+    // subtracts (its entry / pivot) x the pivot row; two barriers per pivot.  At the end row
+    // pivrow[s] is d * [e_s | (M^-1) row s]; each thread divides its own row by its d.
     auto attempt = [&](uint32_t t) -> bool {
       if (tid < m) {       // thread q builds row q: coefficients of the missing sources | identity
         const uint32_t rq = (tid + 1 < m) ? recv[tid] : recv[t];
@@ -1416,33 +1430,32 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         }
       }
       __syncthreads();
+      bool used = false;
+      uint32_t mycol = 0;
       for (uint32_t p = 0; p < m && !(a.ablate & 32u); ++p) {   // bit 32: timing ablation
-        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
-        __syncthreads();
-        if (tid >= p && tid < m && byte_at(tid, p) != 0) atomicMin(&wcnt[4], tid);
-        __syncthreads();
-        const uint32_t q = wcnt[4];
-        if (q == 0xFFFFFFFFu) return false;           // uniform
-        if (q != p) {
-          for (uint32_t w = tid; w < nw; w += 256) {
-            const uint32_t tmp = A[(p) * P + (w)];
-            A[(p) * P + (w)] = A[(q) * P + (w)];
-            A[(q) * P + (w)] = tmp;
-          }
-          __syncthreads();
-        }
-        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(p, p))];
-        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
-        for (uint32_t w = tid; w < nw; w += 256) A[(p) * P + (w)] = mul4(tinv, A[(p) * P + (w)]);
-        __syncthreads();
-        const uint32_t fa = (tid < m && tid != p) ? byte_at(tid, p) : 0u;
-        if (fa != 0) {
+        const uint32_t x = (tid < m) ? byte_at(tid, p) : 0u;
+        const uint32_t q = vote(tid < m && !used && x != 0, p & 1u);
+        if (q == 0xFFFFFFFFu) return false;           // uniform: singular
+        if (tid == q) {
+          used = true;
+          mycol = p;
+          pivrow[p] = static_cast<uint16_t>(q);
+        } else if (x != 0) {
+          const uint32_t fa = gmul(static_cast<uint8_t>(x), static_cast<uint8_t>(field_inv_dev(byte_at(q, p))));
           const uint32_t* tf0 = ptab[fa];
           const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
-          for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(p) * P + (w)]);
+          for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(q) * P + (w)]);
         }
         __syncthreads();
       }
+      if (tid < m && !(a.ablate & 32u)) {             // normalise: own pivot entry -> 1
+        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(tid, mycol))];
+        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
+        for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] = mul4(tinv, A[(tid) * P + (w)]);
+      } else if (tid < m) {
+        pivrow[tid] = static_cast<uint16_t>(tid);
+      }
+      __syncthreads();
       return true;
     };
     uint32_t t = m - 1;
@@ -1468,46 +1481,31 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         }
       }
       __syncthreads();
-      uint32_t rank = 0;
+      uint32_t rank = 0, par = 0;
+      bool used = false;
       for (uint32_t c = 0; c < m && rank + 1 < m; ++c) {
-        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
-        __syncthreads();
-        if (tid >= rank && tid + 1 < m && byte_at(tid, c) != 0) atomicMin(&wcnt[4], tid);
-        __syncthreads();
-        const uint32_t q = wcnt[4];
+        const uint32_t x = (tid < nrecv && !used) ? byte_at(tid, c) : 0u;
+        const uint32_t q = vote(tid + 1 < m && !used && x != 0, par);
+        par ^= 1u;
         if (q == 0xFFFFFFFFu) continue;               // no pivot in this column (uniform)
-        if (q != rank) {
-          for (uint32_t w = tid; w < nwl; w += 256) {
-            const uint32_t tmp = A[(rank) * P + (w)];
-            A[(rank) * P + (w)] = A[(q) * P + (w)];
-            A[(q) * P + (w)] = tmp;
-          }
-          __syncthreads();
-        }
-        const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(rank, c))];
-        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
-        for (uint32_t w = tid; w < nwl; w += 256) A[(rank) * P + (w)] = mul4(tinv, A[(rank) * P + (w)]);
-        __syncthreads();
-        const uint32_t fa = (tid > rank && tid < nrecv) ? byte_at(tid, c) : 0u;
-        if (fa != 0) {
+        if (tid == q) {
+          used = true;
+        } else if (x != 0) {                          // rows still in play: basis + candidates
+          const uint32_t fa = gmul(static_cast<uint8_t>(x), static_cast<uint8_t>(field_inv_dev(byte_at(q, c))));
           const uint32_t* tf0 = ptab[fa];
           const uint32_t tf[5] = {tf0[0], tf0[1], tf0[2], tf0[3], tf0[4]};
-          for (uint32_t w = 0; w < nwl; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(rank) * P + (w)]);
+          for (uint32_t w = 0; w < nwl; ++w) A[(tid) * P + (w)] ^= mul4(tf, A[(q) * P + (w)]);
         }
         __syncthreads();
         ++rank;
       }
       uint32_t next = nrecv;
       if (rank + 1 == m) {
-        if (tid == 0) wcnt[4] = 0xFFFFFFFFu;
-        __syncthreads();
-        if (tid + 1 >= m && tid < nrecv) {
-          uint32_t nz = 0;
+        uint32_t nz = 0;
+        if (tid + 1 >= m && tid < nrecv)
           for (uint32_t w = 0; w < nwl; ++w) nz |= A[(tid) * P + (w)];
-          if (nz != 0) atomicMin(&wcnt[4], tid);
-        }
-        __syncthreads();
-        next = wcnt[4] != 0xFFFFFFFFu ? wcnt[4] : nrecv;
+        const uint32_t v = vote(nz != 0, par);
+        next = v != 0xFFFFFFFFu ? v : nrecv;
       }
       __syncthreads();
       if (next < nrecv) {
@@ -1532,7 +1530,7 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
       uint8_t* pc = a.plan_coef + static_cast<size_t>(g) * k * rp;
       uint16_t* pout = a.plan_out + static_cast<size_t>(g) * rp;
       uint16_t* slen = a.src_len + static_cast<size_t>(g) * k;
-      auto minv = [&](uint32_t s, uint32_t q) -> uint32_t { return byte_at(s, m + q); };
+      auto minv = [&](uint32_t s, uint32_t q) -> uint32_t { return byte_at(pivrow[s], m + q); };
       for (uint32_t s = tid; s < rp; s += 256) pout[s] = (s < m) ? miss[s] : 0;
       // positions 0 .. m-1: the chosen repairs, D[s][q] = (M^-1)[s][q]; thread = output row s
       for (uint32_t q = 0; q < m; ++q) {
@@ -1615,8 +1613,8 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
 // (big_rows * big_pitch is padded to a multiple of 4 dwords, so ptab stays 16-byte aligned)
 inline size_t big_lds_bytes(uint32_t rows, uint32_t pitch, uint32_t mmax)
 {
-  // A, miss/recv/reps/rl/sl (5 x 256 u16), szs, wcnt, v_perm tables, c4 [mmax][8]
-  return (static_cast<size_t>(rows) * pitch + 5 * 128 + 256 + 8 + 256 * 8 + mmax * 8) * 4;
+  // A, miss/recv/reps/rl/sl/pivrow (6 x 256 u16), szs, wcnt + wmin, v_perm tables, c4 [mmax][8]
+  return (static_cast<size_t>(rows) * pitch + 6 * 128 + 256 + 16 + 256 * 8 + mmax * 8) * 4;
 }
 
 // ------------------------------------------------------------- decode plan, r <= 32 (v2) ----

@@ -1900,7 +1900,21 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q);
             uint32_t tc[5];
             tab(((R1 + Sj) * R1) % 255u + 1u, tc);
-            const uint32_t (*sq)[W] = minvS[q];
+            // column q's selector words: 3 x W dwords, read whole (16-byte broadcast loads;
+            // words past m are unused)
+            uint32_t sq[3][W];
+            if constexpr ((3 * W) % 4 == 0) {     // rows of 16-byte multiples (RM >= 16)
+              const u32x4* sq4 = reinterpret_cast<const u32x4*>(&minvS[q][0][0]);
+#pragma unroll
+              for (int e = 0; e < 3 * W / 4; ++e) {
+                const u32x4 v4 = sq4[e];
+#pragma unroll
+                for (int f = 0; f < 4; ++f) sq[(4 * e + f) / W][(4 * e + f) % W] = v4[f];
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 3 * W; ++e) sq[e / W][e % W] = minvS[q][e / W][e % W];
+            }
 #pragma unroll
             for (int w = 0; w < W; ++w)
               if (4u * w < m)

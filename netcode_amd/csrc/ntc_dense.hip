@@ -105,7 +105,7 @@ __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
   __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
   __shared__ uint32_t cmask[3];
   __shared__ uint32_t crow[2][16];
-  __shared__ uint32_t cbuf[2][16][9];                                 // published pivot windows
+  __shared__ __attribute__((aligned(16))) u32x4 cbuf[2][16][9];     // {value, sel_a, sel_b, sel_e}
 
   const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
   for (uint32_t e = i; e < 256 * 8; e += blockDim.x) {
@@ -157,7 +157,15 @@ __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
       const uint32_t fc = __builtin_amdgcn_readlane(f, first);
       const u32x4 ti = *reinterpret_cast<const u32x4*>(&pinv_t[fc][0]);
       const uint32_t ti4 = pinv_t[fc][4];
-      if (lane < 9) cbuf[par][w][lane] = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
+      if (lane < 9) {
+        const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
+        u32x4 o;
+        o[0] = nv;
+        o[1] = nv & 0x07070707u;
+        o[2] = (nv >> 3) & 0x07070707u;
+        o[3] = (nv >> 6) & 0x03030303u;
+        cbuf[par][w][lane] = o;
+      }
       if (lane == 0) {
         crow[par][w] = w * 64u + first;
         atomicOr(&cmask[t % 3], 1u << w);
@@ -170,20 +178,18 @@ __global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
     const uint32_t ws = __ffs(m) - 1;                  // lowest wave = lowest row index
     const uint32_t prow = crow[par][ws];
     if (i == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + t] = prow;
-    // the pivot window: 9 broadcast dword reads (the v_perm selectors are derived here, so the
-    // LDS returns 4 bytes per lane and dword instead of 16)
     if (i == prow) {
       chosen = true;
       elig = false;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) v[wd(e)] = cbuf[par][ws][e];
+      for (int e = 0; e < 9; ++e) v[wd(e)] = cbuf[par][ws][e][0];
     } else if (f != 0) {
 #pragma unroll
       for (int e = 0; e < 9; ++e) {
-        const uint32_t c = cbuf[par][ws][e];
-        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c & 0x07070707u),
-                                               __builtin_amdgcn_perm(tf[3], tf[2], (c >> 3) & 0x07070707u), 0x96) ^
-                   __builtin_amdgcn_perm(tf4, tf4, (c >> 6) & 0x03030303u);
+        const u32x4 c4 = cbuf[par][ws][e];
+        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                               __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
+                   __builtin_amdgcn_perm(tf4, tf4, c4[3]);
       }
     }
   }

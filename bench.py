@@ -322,6 +322,17 @@ def cpu_baseline(k, r, S, stride, m, threads, budget_s=12.0):
     try:
         v1, s1, e1, d1 = cpu_baseline_run(k, r, S, stride, m, 1, budget_s / 3)
         vn, sn, en, dn = cpu_baseline_run(k, r, S, stride, m, threads, budget_s * 2 / 3)
+        gfni = None
+        if L.or_have_gfni():
+            # labelled upper bound: GFNI affine-matrix region MACs, AVX-512
+            L.or_set_simd(2)
+            g1 = cpu_baseline_run(k, r, S, stride, m, 1, budget_s / 6)
+            gn = cpu_baseline_run(k, r, S, stride, m, threads, budget_s / 3)
+            gfni = {"value": round(gn[0], 3), "unit": "GiB/s", "cores": threads,
+                    "sample": gn[1], "encode_s": round(gn[2], 3), "decode_s": round(gn[3], 3),
+                    "single_core": {"value": round(g1[0], 3), "sample": g1[1]},
+                    "note": "upper-bound leg, not gf-complete's algorithm: the same oracle with "
+                            "each region MAC as gf2p8affineqb over 64-byte vectors"}
     finally:
         L.or_set_simd(0)
     shape = f"k={k} r={r} S={S} m={m}, encode+decode"
@@ -333,6 +344,7 @@ def cpu_baseline(k, r, S, stride, m, threads, budget_s=12.0):
             "encode_s": round(en, 3), "decode_s": round(dn, 3),
             "single_core": {"value": round(v1, 3), "cores": 1, "sample": f"{s1} {shape}",
                             "encode_s": round(e1, 3), "decode_s": round(d1, 3)},
+            "gfni_upper_bound": gfni,
             "cpu_model": model, "nproc": nproc, "usable_cpus": usable}
 
 

@@ -152,7 +152,7 @@ uint32_t or_coefficient(uint32_t repair_id, uint32_t src_id)
   return or_fw_coefficient(g_w, repair_id, src_id);
 }
 
-static int g_simd = 0;   /* CPU-baseline mode: route region ops through the AVX2 kernel */
+static int g_simd = 0;   /* CPU-baseline mode: 1 = AVX2 split-nibble region ops, 2 = GFNI (if present) */
 static void muladd_dispatch(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
 
 void or_set_simd(int on) { gf_init(); g_simd = on; }
@@ -311,13 +311,45 @@ static void muladd_avx2(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
   for (; i < len; ++i) dst[i] ^= row[src[i]];
 }
 int or_have_avx2(void) { return __builtin_cpu_supports("avx2"); }
+
+/* GFNI + AVX-512 region MAC (a labelled CPU upper bound, not gf-complete's
+ * algorithm).  Multiplication by c is GF(2)-linear on the bits of a byte: y_i = XOR_j M[i][j] x_j
+ * with column j = c * 2^j (mod 0x11D); gf2p8affineqb applies such a matrix to 64 bytes at once,
+ * taking row i from byte 7-i of the matrix qword.  (gf2p8mulb is fixed to the AES polynomial
+ * 0x11B, so it cannot be used for netcode's 0x11D field.) */
+__attribute__((target("avx512f,avx512bw,gfni")))
+static void muladd_gfni(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
+{
+  uint64_t A = 0;
+  for (int i = 0; i < 8; ++i) {
+    uint64_t row = 0;
+    for (int j = 0; j < 8; ++j) row |= (uint64_t)((g_mul[c][1u << j] >> i) & 1u) << j;
+    A |= row << (8 * (7 - i));
+  }
+  const __m512i a = _mm512_set1_epi64((long long)A);
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) {
+    const __m512i x = _mm512_loadu_si512((const void*)(src + i));
+    const __m512i d = _mm512_loadu_si512((const void*)(dst + i));
+    _mm512_storeu_si512((void*)(dst + i), _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(x, a, 0)));
+  }
+  const uint8_t* row = g_mul[c];
+  for (; i < len; ++i) dst[i] ^= row[src[i]];
+}
+int or_have_gfni(void)
+{
+  return __builtin_cpu_supports("gfni") && __builtin_cpu_supports("avx512bw") &&
+         __builtin_cpu_supports("avx512f");
+}
 #else
 int or_have_avx2(void) { return 0; }
+int or_have_gfni(void) { return 0; }
 #endif
 
 static void muladd_dispatch(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c)
 {
 #if defined(__x86_64__)
+  if (g_simd == 2 && or_have_gfni()) { muladd_gfni(src, dst, len, c); return; }
   if (or_have_avx2()) { muladd_avx2(src, dst, len, c); return; }
 #endif
   const uint8_t* row = g_mul[c];

@@ -143,6 +143,7 @@ int  or_uniform_next(or_uniform*);       /* 1 = lost */
  * with pshufb); used as the CPU baseline.  Falls back to the scalar loop without AVX2. */
 void or_region_muladd_simd(const uint8_t* src, uint8_t* dst, size_t len, uint8_t c);
 int  or_have_avx2(void);
+int  or_have_gfni(void);               /* GFNI + AVX-512BW region path available (or_set_simd(2)) */
 /* Route the oracle's own region ops through the AVX2 kernel (CPU baseline timing only). */
 void or_set_simd(int on);
 

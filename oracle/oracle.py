@@ -107,6 +107,7 @@ def lib():
         L.or_decoder_counter.restype = C.c_size_t
         L.or_decoder_counter.argtypes = [P, C.c_int]
         L.or_have_avx2.restype = C.c_int
+        L.or_have_gfni.restype = C.c_int
         L.or_set_simd.argtypes = [C.c_int]
         L.or_write_repair_packet.restype = C.c_size_t
         L.or_write_repair_packet.argtypes = [C.c_uint32, P, C.c_uint16, P, C.c_size_t, C.c_uint16, P]

@@ -112,6 +112,29 @@ def test_simd_region_matches_scalar(oracle):
             assert (d0 == d1).all()
 
 
+def test_gfni_region_matches_scalar(oracle):
+    """The GFNI affine-matrix region MAC (the CPU upper-bound leg; or_set_simd(2)) gives the
+    scalar 0x11D products for every coefficient."""
+    L = oracle.lib()
+    if not L.or_have_gfni():
+        pytest.skip("no GFNI / AVX-512BW on this CPU")
+    rng = np.random.default_rng(1)
+    L.or_set_simd(2)
+    try:
+        for n in [0, 1, 63, 64, 65, 1000, 4096]:
+            src = rng.integers(0, 256, n + 1, dtype=np.uint8)
+            for c in range(256):
+                d0 = rng.integers(0, 256, n + 1, dtype=np.uint8)
+                d1 = d0.copy()
+                L.or_set_simd(0)
+                L.or_region_muladd(oracle._p(src), oracle._p(d0), n, c)
+                L.or_set_simd(2)
+                L.or_region_muladd(oracle._p(src), oracle._p(d1), n, c)
+                assert (d0 == d1).all(), (n, c)
+    finally:
+        L.or_set_simd(0)
+
+
 def test_generation_decode_round_trip_and_states(oracle):
     from helpers import loss_exact_m, make_sources
     G, k, r, S = 20, 32, 8, 256

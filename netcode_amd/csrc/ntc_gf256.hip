@@ -492,6 +492,12 @@ __device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, ui
 // source, 8-row tile), 8 u16 block offsets (kGxOff[c] of the tile's rows) instead of the nibble-
 // site jump offsets.  GX = 2: the chain reads the coefficient bytes a.coef [G][k][rp] directly
 // (8 rows = one u64 per source).  R must be 8 (fewer rows carry c = 0, which the chains skip).
+// Lean entry into the shared table (tuning switch, NTC_GX_LEAN=0 builds the original entry)
+#ifndef NTC_GX_LEAN
+#define NTC_GX_LEAN 1
+#endif
+constexpr bool kGxLean = NTC_GX_LEAN != 0;
+
 template <int R, int RT, bool DEC, int ABL = 0, int GX = 0>
 __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
                                             uint32_t nrows, uint32_t cc, uint32_t lane,
@@ -625,6 +631,24 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     } else if constexpr (GX == 2) {
       const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
       asm volatile(NTC_GX2_CHAIN : NTC_GX_OUTS(A) : NTC_GX2_INS(Y, P) : NTC_GX2_CLOBBERS);
+      continue;
+    } else if constexpr (GX == 3 && kGxLean) {
+      // lean entry: the coefficient pair and the table base arrive in the registers the chain
+      // uses (s[90:91], s[96:97]), and an all-zero pair needs no test (its block 0 has no VALU
+      // and its tail returns at once).  M0 (compiler-reserved) is still saved and restored.
+      uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
+      asm volatile("s_mov_b32 s94, m0\n"
+                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                   "s_lshl_b32 s98, s90, 24\n"
+                   "s_lshr_b32 s98, s98, 17\n"
+                   "s_add_u32 s98, s96, s98\n"
+                   "s_addc_u32 s99, s97, 0\n"
+                   "s_swappc_b64 s[92:93], s[98:99]\n"
+                   "s_set_gpr_idx_off\n"
+                   "s_mov_b32 m0, s94\n"
+                   : NTC_GX_OUTS(A), [p] "+{s[90:91]}"(P)
+                   : NTC_GX3_YPINS(Y), [tb] "{s[96:97]}"(tbase)
+                   : "s92", "s93", "s94", "s98", "s99", "scc");
       continue;
     } else if constexpr (GX == 3) {
       const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;

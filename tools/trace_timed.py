@@ -2,10 +2,10 @@
 bench's own HIP-event numbers (bench.py roofline.kernel_ms / kernels_ms).  rocprofv3 --stats
 averages every launch of the profiled process, warmup included (the first launches run while the
 clocks ramp up); the bench times only the last `--steps` steps.  This takes, per kernel name, the
-last `timed` launches (default: steps x launches per step = the trailing launches) and prints
-their mean next to the all-launch mean.
+launches of the last `timed` of `total` steps and prints their time per step next to the
+all-launch mean (a split batch launches its MAC twice per step).
 
-usage: python tools/trace_timed.py <run_kernel_trace.csv> --timed 10 [--bench <bench log>]
+usage: python tools/trace_timed.py <run_kernel_trace.csv> --timed 10 --total 40 [--bench <bench log>]
 """
 import argparse
 import csv
@@ -21,7 +21,8 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--timed", type=int, required=True, help="launches per kernel in the timed steps")
+    ap.add_argument("--timed", type=int, required=True, help="timed steps (the trailing ones)")
+    ap.add_argument("--total", type=int, required=True, help="steps in the run (warmup + timed)")
     ap.add_argument("--bench", help="bench log whose JSON line to compare against")
     a = ap.parse_args()
     per = {}
@@ -32,12 +33,15 @@ def main():
     for n, v in per.items():
         v.sort()
         ds = [d for _, d in v]
-        if len(ds) < a.timed or not n.startswith(("gf_", "decode_plan", "encode_prep", "plan_rows",
+        if len(ds) < a.total or not n.startswith(("gf_", "decode_plan", "encode_prep", "plan_rows",
                                                      "bj_offsets", "dense", "slot_pack", "wire_")):
             continue
-        out[n] = {"launches": len(ds), "mean_all_ms": round(sum(ds) / len(ds), 4),
-                  "mean_timed_ms": round(sum(ds[-a.timed:]) / a.timed, 4)}
-    res = {"kernels": out, "timed_launches_per_kernel": a.timed}
+        lps = len(ds) // a.total                       # launches per step
+        tail = ds[-a.timed * lps:]
+        out[n] = {"launches": len(ds), "launches_per_step": lps,
+                  "mean_all_launches_ms": round(sum(ds) / len(ds), 4),
+                  "timed_ms_per_step": round(sum(tail) / a.timed, 4)}
+    res = {"kernels": out, "timed_steps": a.timed, "total_steps": a.total}
     if a.bench:
         for line in open(a.bench):
             if line.startswith("{"):

@@ -1821,6 +1821,70 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         v |= 1u << (8u * ((lane - m) & 3u));
       orig[w] = v;
     }
+    // After a singular first candidate: rank screening instead of one Gauss-Jordan per further
+    // candidate (decoder.cc:448-468 tries t = m, m+1, ... in turn).  {first m-1 repairs} + {t} is
+    // invertible iff the first m-1 rows are independent and row t lies outside their span: a
+    // forward elimination of all received rows over the m missing columns (lane = row, rows in
+    // this wave's minvS scratch, free until a plan is emitted), pivots from rows 0..m-2 only,
+    // leaves each candidate reduced against that basis; the first nonzero one is where the
+    // reference stops.  Returns that candidate's index, or nrecv when every candidate fails.
+    auto screen_candidates = [&]() -> uint32_t {
+      constexpr uint32_t SP = W + 1;                   // odd dword pitch
+      uint32_t* S = &minvS[0][0][0];
+      const uint32_t nwl = (m + 3) / 4;
+      if (lane < nrecv) {
+        for (uint32_t w = 0; w < nwl; ++w) {
+          uint32_t word = 0;
+          for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t c = 4 * w + b;
+            if (c < m) {
+              const uint32_t S1c = __builtin_amdgcn_readlane(S1, c);
+              word |= (((rid1 + S1c) * rid1) % 255u + 1u) << (8 * b);
+            }
+          }
+          S[lane * SP + w] = word;
+        }
+      }
+      wave_sync();
+      uint32_t rank = 0;
+      for (uint32_t c = 0; c < m && rank + 1 < m; ++c) {
+        const uint32_t cw = c >> 2, cs = 8 * (c & 3);
+        const uint32_t f = lane < nrecv ? (S[lane * SP + cw] >> cs) & 0xFFu : 0u;
+        const uint64_t b = __ballot(lane >= rank && lane + 1 < m && f != 0);
+        if (b == 0) continue;                          // no pivot in this column (uniform)
+        const uint32_t q = __ffsll(static_cast<unsigned long long>(b)) - 1;
+        if (q != rank) {
+          if (lane < nwl) {
+            const uint32_t tmp = S[rank * SP + lane];
+            S[rank * SP + lane] = S[q * SP + lane];
+            S[q * SP + lane] = tmp;
+          }
+          wave_sync();
+        }
+        const uint32_t* ti = d_pinv.w[(S[rank * SP + cw] >> cs) & 0xFFu];
+        const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
+        if (lane < nwl) S[rank * SP + lane] = mul4(tinv, S[rank * SP + lane]);
+        wave_sync();
+        const uint32_t fa = (lane > rank && lane < nrecv) ? (S[lane * SP + cw] >> cs) & 0xFFu : 0u;
+        if (fa != 0) {
+          uint32_t tf[5];
+          tab(fa, tf);
+          for (uint32_t w = 0; w < nwl; ++w) S[lane * SP + w] ^= mul4(tf, S[rank * SP + w]);
+        }
+        wave_sync();
+        ++rank;
+      }
+      uint32_t next = nrecv;
+      if (rank + 1 == m) {
+        uint32_t nz = 0;
+        if (lane + 1 >= m && lane < nrecv)
+          for (uint32_t w = 0; w < nwl; ++w) nz |= S[lane * SP + w];
+        const uint64_t b = __ballot(nz != 0);
+        if (b != 0) next = __ffsll(static_cast<unsigned long long>(b)) - 1;
+      }
+      wave_sync();
+      return next;
+    };
     uint32_t col[W];
     bool ok = false;
     uint32_t t = m - 1;
@@ -1831,6 +1895,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       for (int w = 0; w < W; ++w) col[w] = orig[w];
       set_byte_dyn<W>(col, m - 1, ct | byte_dyn<W>(orig, m - 1));
       if ((a.ablate & 1u) || gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
+      if (t == m - 1 && t + 1 < nrecv) t = screen_candidates() - 1;   // the loop's ++t: next
     }
     if (!ok) {
       st.state = 3;

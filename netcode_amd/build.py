@@ -66,6 +66,8 @@ OUT_DIR = os.path.join(ROOT, "tests", "_build")
 CPP_CHECKS = {
     "cpp_surface_test": (["tests/cpp/cpp_surface_test.cc"], False),
     "detail_packetizer_test": (["tests/cpp/detail_packetizer_test.cc"], False),
+    # bench.py --per-packet: the C-level per-packet workload over libntc.so
+    "pp_driver": (["tools/pp_driver.c"], False),
     "ref_cpp_basic": ([REF + "/examples/basic/cpp_basic.cc"], True),
     "ref_c_basic": ([REF + "/examples/basic/c_basic.c"], True),
     "ref_end_to_end": ([REF + "/tests/end_to_end.cc"], True),

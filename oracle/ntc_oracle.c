@@ -1519,3 +1519,120 @@ int or_end_to_end(uint32_t nb_packets, uint64_t* out)
   or_decoder_free(dec);
   return bad ? -1 : 0;
 }
+
+/* ================================================ per-packet workload (CPU baseline leg) ==== */
+/* bench.py --per-packet, C level: F flows x M items of S bytes through one ntc::encoder per flow
+ * (window W, a repair every R sources), then each flow's packets with an i.i.d. loss of L % fed to
+ * its own in-order decoder, round-robin over flows -- the reference's usage, one call per packet.
+ * The GPU side (tools/pp_driver.c over libntc.so) draws the same payloads and losses, so both
+ * produce the same packets and deliveries (hashes compared).  Timed: the encode calls, the decode
+ * calls.  secs[0..1] = encode, decode; counts[0..3] = packets, received packets, deliveries,
+ * repairs; hashes[0..1] = FNV-1a over every flow's packets, over every flow's deliveries. */
+static uint64_t pp_mix(uint64_t x)
+{
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+static uint64_t pp_fnv(uint64_t h, const uint8_t* p, size_t n)
+{
+  for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  return h;
+}
+
+typedef struct { uint8_t* v; size_t n, cap; size_t* off; size_t np, capp; } pp_store;
+
+static void pp_push(pp_store* s, const uint8_t* p, size_t n)
+{
+  if (s->n + n > s->cap) {
+    s->cap = (s->n + n) * 2 + 4096;
+    s->v = (uint8_t*)realloc(s->v, s->cap);
+  }
+  if (s->np + 2 > s->capp) {
+    s->capp = s->capp * 2 + 64;
+    s->off = (size_t*)realloc(s->off, s->capp * sizeof(size_t));
+  }
+  if (s->np == 0) s->off[0] = 0;
+  memcpy(s->v + s->n, p, n);
+  s->n += n;
+  s->off[++s->np] = s->n;
+}
+
+static void pp_emit(void* ctx, const uint8_t* p, size_t n) { pp_push((pp_store*)ctx, p, n); }
+static void pp_deliver(void* ctx, uint32_t id, const uint8_t* p, size_t n)
+{
+  (void)id;
+  pp_push((pp_store*)ctx, p, n);
+}
+
+static double pp_now(void)
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+int or_pp_bench(uint32_t F, uint32_t M, uint32_t S, uint32_t W, uint32_t R, uint32_t loss_pct,
+                uint64_t seed, double* secs, uint64_t* counts, uint64_t* hashes)
+{
+  gf_init();
+  uint8_t* data = (uint8_t*)malloc((size_t)M * S + 8);
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t b = 0; b < S; ++b)
+      data[(size_t)i * S + b] = (uint8_t)(pp_mix(seed + ((uint64_t)i << 32) + b / 8) >> (8 * (b % 8)));
+  pp_store* tx = (pp_store*)calloc(F, sizeof(pp_store));
+  pp_store* rx = (pp_store*)calloc(F, sizeof(pp_store));
+  pp_store* acks = (pp_store*)calloc(F, sizeof(pp_store));
+  or_encoder** enc = (or_encoder**)calloc(F, sizeof(or_encoder*));
+  or_decoder** dec = (or_decoder**)calloc(F, sizeof(or_decoder*));
+  for (uint32_t f = 0; f < F; ++f) {
+    enc[f] = or_encoder_new(pp_emit, &tx[f]);
+    or_encoder_set_rate(enc[f], R);
+    or_encoder_set_window_size(enc[f], W);
+  }
+  double t0 = pp_now();
+  for (uint32_t i = 0; i < M; ++i)
+    for (uint32_t f = 0; f < F; ++f) or_encoder_add_data(enc[f], data + (size_t)i * S, (uint16_t)S);
+  secs[0] = pp_now() - t0;
+  uint64_t npk = 0, nrep = 0, nrx = 0, ndel = 0;
+  for (uint32_t f = 0; f < F; ++f) { npk += tx[f].np; nrep += or_encoder_nb_sent_repairs(enc[f]); }
+  /* the received streams: packet j of flow f survives iff mix(seed, f, j) % 100 >= loss_pct */
+  uint32_t** keep = (uint32_t**)calloc(F, sizeof(uint32_t*));
+  uint32_t* nkeep = (uint32_t*)calloc(F, sizeof(uint32_t));
+  uint32_t rounds = 0;
+  for (uint32_t f = 0; f < F; ++f) {
+    keep[f] = (uint32_t*)malloc((tx[f].np + 1) * sizeof(uint32_t));
+    for (uint32_t j = 0; j < tx[f].np; ++j)
+      if (pp_mix(seed ^ 0x5EEDull ^ ((uint64_t)f << 40) ^ j) % 100 >= loss_pct) keep[f][nkeep[f]++] = j;
+    nrx += nkeep[f];
+    if (nkeep[f] > rounds) rounds = nkeep[f];
+    dec[f] = or_decoder_new(1, pp_emit, &acks[f], pp_deliver, &rx[f]);
+    or_decoder_set_ack_period_ms(dec[f], 0);
+  }
+  t0 = pp_now();
+  for (uint32_t i = 0; i < rounds; ++i)
+    for (uint32_t f = 0; f < F; ++f)
+      if (i < nkeep[f]) {
+        const uint32_t j = keep[f][i];
+        or_decoder_add_packet(dec[f], tx[f].v + tx[f].off[j], tx[f].off[j + 1] - tx[f].off[j]);
+      }
+  secs[1] = pp_now() - t0;
+  uint64_t hp = 0xCBF29CE484222325ull, hd = 0xCBF29CE484222325ull;
+  for (uint32_t f = 0; f < F; ++f) {
+    hp = pp_fnv(hp, tx[f].v, tx[f].n);
+    hd = pp_fnv(hd, rx[f].v, rx[f].n);
+    ndel += rx[f].np;
+  }
+  counts[0] = npk; counts[1] = nrx; counts[2] = ndel; counts[3] = nrep;
+  hashes[0] = hp; hashes[1] = hd;
+  for (uint32_t f = 0; f < F; ++f) {
+    or_encoder_free(enc[f]);
+    or_decoder_free(dec[f]);
+    free(tx[f].v); free(tx[f].off); free(rx[f].v); free(rx[f].off);
+    free(acks[f].v); free(acks[f].off); free(keep[f]);
+  }
+  free(tx); free(rx); free(acks); free(enc); free(dec); free(keep); free(nkeep); free(data);
+  return 0;
+}

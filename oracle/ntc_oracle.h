@@ -168,6 +168,10 @@ int or_read_packet_into(const uint8_t* pkt, size_t len, uint32_t G, uint32_t k, 
                         uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
                         uint8_t* rep_mask);
 
+/* bench.py --per-packet CPU leg (C level): see ntc_oracle.c.  secs[2], counts[4], hashes[2]. */
+int or_pp_bench(uint32_t flows, uint32_t items, uint32_t size, uint32_t window, uint32_t rate,
+                uint32_t loss_pct, uint64_t seed, double* secs, uint64_t* counts, uint64_t* hashes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -108,6 +108,7 @@ def lib():
         L.or_decoder_counter.argtypes = [P, C.c_int]
         L.or_have_avx2.restype = C.c_int
         L.or_have_gfni.restype = C.c_int
+        L.or_pp_bench.argtypes = [C.c_uint32] * 6 + [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_set_simd.argtypes = [C.c_int]
         L.or_write_repair_packet.restype = C.c_size_t
         L.or_write_repair_packet.argtypes = [C.c_uint32, P, C.c_uint16, P, C.c_size_t, C.c_uint16, P]

@@ -143,3 +143,25 @@ def test_rejects_wrong_packet_types(capi):
     with pytest.raises(capi.NtcError) as e:
         dec.add_packet(bytes.fromhex("0200000000ffff61"))   # declared length past the end
     assert e.value.kind == "overflow_error"
+
+
+@pytest.mark.parametrize("mode", ["immediate", "batched"])
+@pytest.mark.parametrize("flows,items,size,window,rate,loss", [(16, 24, 1024, 32, 4, 10),
+                                                               (5, 40, 300, 8, 2, 30)])
+def test_c_level_per_packet_matches_oracle(oracle, mode, flows, items, size, window, rate, loss):
+    """tools/pp_driver.c (bench.py --per-packet's C-level GPU leg: one encoder / decoder per
+    flow through the reference C ABI, immediate or batched) produces exactly the packets and the
+    deliveries of the oracle's or_pp_bench on the same payload and loss draws."""
+    import ctypes as C
+    import subprocess
+    drv = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "_build",
+                       "pp_driver")
+    args = [str(x) for x in (flows, items, size, window, rate, loss, 11)]
+    r = subprocess.run([drv, mode] + args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    g = json.loads(r.stdout.strip().splitlines()[-1])
+    secs, cnt, hs = (C.c_double * 2)(), (C.c_uint64 * 4)(), (C.c_uint64 * 2)()
+    assert oracle.lib().or_pp_bench(flows, items, size, window, rate, loss, C.c_uint64(11), secs, cnt, hs) == 0
+    assert [g["packets"], g["received"], g["deliveries"], g["repairs"]] == list(cnt)
+    assert g["packets_hash"] == f"{hs[0]:016x}"
+    assert g["deliveries_hash"] == f"{hs[1]:016x}"

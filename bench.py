@@ -668,7 +668,12 @@ def main():
     achieved = bytes_dom / (t_dom * 1e-3) / 1e9
     traffic, tsrc = pmc_record("pmc_traffic.json", a.config, dom)
     valu, vsrc = pmc_record("pmc_valu.json", a.config, dom)
-    ksum = sum(kern.values())
+    # per-step kernel times: the MAC kernels from the timed steps themselves, the others (prep,
+    # plan, row pointers, dense inversion) from the logged warmup steps
+    kern_step = dict(kern)
+    kern_step["encode_mac"] = t_emac
+    kern_step["decode_mac"] = t_dmac
+    ksum = sum(kern_step.values())
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": tsrc, "kernel": dom, "kernel_ms": round(t_dom, 4),
@@ -692,10 +697,12 @@ def main():
                           f"{G - ndec} of {G} per rank are singular under the reference "
                           "coefficient schedule (encoded and planned, no decode MAC)",
             "roofline": roof,
-            "kernels_ms": {n: round(v, 4) for n, v in sorted(kern.items())},
-            "kernels_ms_note": f"per step, summed over that step's launches; from the last {nb} "
-                               f"warmup steps, run with every launch bracketed by events "
-                               f"({ms_logged:.4f} ms per step there)",
+            "kernels_ms": {n: round(v, 4) for n, v in sorted(kern_step.items())},
+            "kernels_ms_note": f"per step: encode_mac / decode_mac from the timed steps (HIP "
+                               f"events on every MAC launch), the other kernels from the last "
+                               f"{nb} warmup steps, run with every launch bracketed",
+            "kernels_ms_warmup_logged": {n: round(v, 4) for n, v in sorted(kern.items())},
+            "ms_per_step_warmup_logged": round(ms_logged, 4),
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_step),
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}

@@ -576,10 +576,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; NTC_BENCH_BACKEND=gloo lets a test run several ranks on fewer GPUs
+    # (ranks then share devices round-robin), RCCL ("nccl") otherwise
+    backend = os.environ.get("NTC_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if (backend == "gloo" and ndev) else local
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     k, r, S, stride, m, Gdef = CONFIGS[a.config]

@@ -25,6 +25,10 @@ struct ntc_gf256_engine {
   void* joff_dec = nullptr;    // decode offsets written by decode_plan (ntc_gf256_decode_batch)
   size_t joff_dec_cap = 0;
   bool last_plan_offsets = false;
+  // the last plan also wrote the decode MAC's input row addresses (row_ptr) for these buffers
+  const uint8_t* rows_src = nullptr;
+  const uint8_t* rows_rep = nullptr;
+  uint32_t rows_stride = 0;
   void* row_ptr = nullptr;     // bit-sliced decode: input row address per plan position
   size_t row_ptr_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;

@@ -964,6 +964,12 @@ struct PlanArgs {
   uint32_t* joff;    // non-null: also write the bit-sliced MAC's jump offsets (8-row tiles)
   uint32_t ntiles;
   uint32_t big_rows, big_pitch;   // decode_plan_big: LDS matrix shape
+  // decode_plan_w, when non-null: also write the decode MAC's input row addresses (what
+  // plan_rows computes at apply time) for the buffers the apply will use
+  uint64_t* rows_out;
+  const uint8_t* rows_src;
+  const uint8_t* rows_rep;
+  uint64_t rows_stride;
   uint32_t m_cap;                 // decode_plan_big: > 0: defer generations with m > m_cap
   uint32_t deferred_only;         // decode_plan_big: only the generations an m_cap pass deferred
 };
@@ -1953,6 +1959,16 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
                           __builtin_amdgcn_perm(th[4], th[4], s2));
           }
       };
+      // input row address of plan position `pos` (plan_rows' layout: k entries, then kBjRing
+      // copies of the last one, read by the MAC's prefetch)
+      uint64_t* rows_g = a.rows_out ? a.rows_out + static_cast<size_t>(g) * (k + kBjRing) : nullptr;
+      auto put_row = [&](uint32_t pos, const uint8_t* row) {
+        if (!rows_g) return;
+        const uint64_t v = reinterpret_cast<uint64_t>(row);
+        rows_g[pos] = v;
+        if (pos == k - 1)
+          for (uint32_t e = 0; e < static_cast<uint32_t>(kBjRing); ++e) rows_g[k + e] = v;
+      };
       // R1 of the repair in row q (rows 0 .. m-2: received repairs 0 .. m-2; row m-1: repair t)
       const uint32_t t_rid1 = __builtin_amdgcn_readlane(rid1, t);
       const uint32_t row_r1 = (lane == m - 1) ? t_rid1 : rid1;
@@ -1961,6 +1977,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         const uint32_t q = lane - m;
         const uint32_t rq = (q + 1 < m) ? recv[q] : recv[t];
         pin[q] = static_cast<uint16_t>(k + rq);
+        put_row(q, a.rows_rep + (static_cast<uint64_t>(g) * r + rq) * a.rows_stride);
         emit(q, col);
 #pragma unroll
         for (int w = 0; w < W; ++w) {
@@ -1981,6 +1998,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         if (got) {
           const uint32_t pos = pos_base + __popcll(b & lt);
           pin[pos] = static_cast<uint16_t>(j);
+          put_row(pos, a.rows_src + (static_cast<uint64_t>(g) * k + j) * a.rows_stride);
           const uint32_t Sj = sidb + j + 1u;
           uint32_t acc[W];
 #pragma unroll
@@ -2168,7 +2186,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
        : gv == 2 ? (dec ? gf_mac_bj<8, true, 0, 2> : gf_mac_bj<8, false, 0, 2>)
                  : (dec ? gf_mac_bj<8, true, 0, 1> : gf_mac_bj<8, false, 0, 1>);
     a.ntiles = (a.rows + 7) / 8;
-    if (dec) {
+    if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
       if (rc) return rc;
@@ -2536,10 +2554,14 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   return launch_mac(e, false, a, st, "encode_mac launch", fused);
 }
 
+// rows_src / rows_rep (decode_batch, which knows the apply's buffers): a register plan also
+// writes the decode MAC's input row addresses, so the apply skips plan_rows.
 static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, uint16_t* src_len,
                      const uint8_t* src_mask, const uint16_t* rep_size, const uint8_t* rep_mask,
                      const uint32_t* sid_base, const uint32_t* rid_base,
-                     ntc_gf256_decode_status* status, void* stream, bool offsets)
+                     ntc_gf256_decode_status* status, void* stream, bool offsets,
+                     const uint8_t* rows_src = nullptr, const uint8_t* rows_rep = nullptr,
+                     uint32_t rows_stride = 0)
 {
   if (!e || !src_len || !src_mask || !rep_size || !rep_mask || !status)
     return fail(NTC_GPU_EINVAL, "NULL argument");
@@ -2611,6 +2633,15 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     }
   } else if (r <= 32 && !lds_plan && !ablate) {
     p.ablate = ablate_w;
+    if (rows_src && rows_rep && use_bitslice(e, rows_stride) && gx_chain()) {
+      rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<uint64_t>(G) * (k + kBjRing) * 8,
+                      "hipMalloc row_ptr");
+      if (rc) return rc;
+      p.rows_out = static_cast<uint64_t*>(e->row_ptr);
+      p.rows_src = rows_src;
+      p.rows_rep = rows_rep;
+      p.rows_stride = rows_stride;
+    }
     auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;
     hipLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,
                        static_cast<hipStream_t>(stream), p);
@@ -2620,6 +2651,9 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
   }
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
   e->last_plan_offsets = p.joff != nullptr;
+  e->rows_src = p.rows_out ? rows_src : nullptr;
+  e->rows_rep = p.rows_out ? rows_rep : nullptr;
+  e->rows_stride = p.rows_out ? rows_stride : 0;
   return hip_check(hipGetLastError(), "decode_plan launch");
 }
 
@@ -2658,6 +2692,9 @@ int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   a.coef = e->plan_coef; a.rp = e->last_rp;
   const bool ready = e->last_plan_offsets && bitslice_rt8(e, stride);
   if (ready) a.joff = static_cast<const uint32_t*>(e->joff_dec);
+  // row addresses already written by the plan for exactly these buffers
+  if (e->rows_src == src && e->rows_rep == rep && e->rows_stride == stride && src)
+    a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
   return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch", ready);
 }
 
@@ -2669,9 +2706,10 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
 {
   int rc = check_shape(G, k, r, stride);
   if (rc) return rc;
-  // the plan also writes the bit-sliced MAC's jump offsets when the apply will use them
+  // the plan also writes the bit-sliced MAC's jump offsets when the apply will use them, and
+  // (register plan, shared-table MAC) the MAC's input row addresses
   rc = plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
-                 stream, bitslice_rt8(e, stride));
+                 stream, bitslice_rt8(e, stride), src, rep, stride);
   if (rc) return rc;
   return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
 }

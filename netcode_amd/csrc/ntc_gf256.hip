@@ -586,6 +586,8 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     vm_wait<2 * (kBjRing - 2)>();
     ring_read(ring_p, lane, ycur);
   }
+  uint32_t Yk[kBjPlanes];      // ABL & 2 with the shared table: the tables kept from source 0
+  (void)Yk;
   for (uint32_t i = 0; i < k; ++i) {
     OffV o[NJ];
 #pragma unroll
@@ -619,6 +621,14 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
     next_offsets(i);
     if constexpr (!(ABL & 2)) {
       NTC_BJ_TABLES(Y)
+    } else if constexpr (GX >= 3) {   // timing ablation: source 0's tables for every source
+      if (i == 0) {
+        NTC_BJ_TABLES(Y)
+#pragma unroll
+        for (int n = 8; n < kBjPlanes; ++n) Yk[n] = Y[n];
+      }
+#pragma unroll
+      for (int n = 8; n < kBjPlanes; ++n) Y[n] = Yk[n];
     } else {
 #pragma unroll
       for (int n = 8; n < kBjPlanes; ++n) Y[n] = Y[n & 7] + n;
@@ -2257,6 +2267,16 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     const char* v = std::getenv("NTC_GF256_BJ_ABLATE");
     return v ? std::atoi(v) : 0;
   }();
+  if (ablate && fn == gf_mac_bj<8, false, 0, 3>) {   // timing ablations of the shared-table MAC
+    switch (ablate) {
+      case 1: fn = gf_mac_bj<8, false, 1, 3>; break;
+      case 2: fn = gf_mac_bj<8, false, 2, 3>; break;
+      case 3: fn = gf_mac_bj<8, false, 3, 3>; break;
+      case 64: fn = gf_mac_bj<8, false, 64, 3>; break;
+      case 67: fn = gf_mac_bj<8, false, 67, 3>; break;
+      default: break;
+    }
+  }
   if (ablate && fn == gf_mac_bj<8, false>) {
     switch (ablate) {
       case 1: fn = gf_mac_bj<8, false, 1>; break;

@@ -610,6 +610,9 @@ def main():
     # repetitions (clock ramp experiment, NTC_BENCH_PROBE_FIRST=<reps>)
     probe_reps = int(os.environ.get("NTC_BENCH_PROBE_FIRST", "0"))
     probe = hbm_copy_probe(dev, reps=probe_reps) if probe_reps else None
+    # kernels bracketed by events inside the timed steps: the MACs (plus, for the dense config,
+    # its two inversion/layout launches: 4 ms steps make the event cost negligible)
+    timed_kinds = ("encode_mac", "decode_mac") + (("dense",) if dense else ())
     # the last nb warmup steps run with every kernel bracketed by events (kernels_ms breakdown);
     # the timed steps then log only the MAC kernels (roofline), in the same log
     nb = min(a.warmup, 10)
@@ -623,10 +626,10 @@ def main():
     if nb:
         ms_logged = (time.perf_counter() - tb) / nb * 1e3
         n_breakdown = len(engine.timing_read())
-        engine.timing_kinds(("encode_mac", "decode_mac"))
+        engine.timing_kinds(timed_kinds)
     else:
         ms_logged, n_breakdown = 0.0, 0
-        engine.timing_log(a.steps * 16, kinds=("encode_mac", "decode_mac"))
+        engine.timing_log(a.steps * 16, kinds=timed_kinds)
 
     def barrier():
         if world > 1:
@@ -656,7 +659,7 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     payload = G * k * S * world
     value = payload / (elapsed / a.steps) / 2**30
-    _, launches = kernel_summary(log, a.steps, dense)
+    kern_timed, launches = kernel_summary(log, a.steps, dense)
     kern = kernel_summary(full_log[:n_breakdown], nb, dense)[0] if nb else {}   # logged warmup
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / its mean launch duration
@@ -676,8 +679,7 @@ def main():
     # per-step kernel times: the MAC kernels from the timed steps themselves, the others (prep,
     # plan, row pointers, dense inversion) from the logged warmup steps
     kern_step = dict(kern)
-    kern_step["encode_mac"] = t_emac
-    kern_step["decode_mac"] = t_dmac
+    kern_step.update(kern_timed)
     ksum = sum(kern_step.values())
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
@@ -703,9 +705,9 @@ def main():
                           "coefficient schedule (encoded and planned, no decode MAC)",
             "roofline": roof,
             "kernels_ms": {n: round(v, 4) for n, v in sorted(kern_step.items())},
-            "kernels_ms_note": f"per step: encode_mac / decode_mac from the timed steps (HIP "
-                               f"events on every MAC launch), the other kernels from the last "
-                               f"{nb} warmup steps, run with every launch bracketed",
+            "kernels_ms_note": f"per step: {', '.join(sorted(kern_timed))} from the timed steps "
+                               f"(HIP events on every such launch), the other kernels from the "
+                               f"last {nb} warmup steps, run with every launch bracketed",
             "kernels_ms_warmup_logged": {n: round(v, 4) for n, v in sorted(kern.items())},
             "ms_per_step_warmup_logged": round(ms_logged, 4),
             "kernel_sum_ms_per_step": round(ksum, 4),

@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=30)
     p.add_argument("--config", default="k128r32s4096", choices=sorted(CONFIGS))
     p.add_argument("--G", type=int, default=0, help="generations per GPU (default per config)")
+    p.add_argument("--S", type=int, default=0, help="symbol bytes (exploration; default per config)")
     p.add_argument("--mixed", action="store_true", help="m ~ U[0, r] instead of m = r")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-rate", action="store_true")
@@ -588,6 +589,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     k, r, S, stride, m, Gdef = CONFIGS[a.config]
+    if a.S:
+        S, stride = a.S, (a.S + 15) // 16 * 16
     G = a.G or Gdef
 
     if world == 1:

@@ -67,7 +67,7 @@ int  ntc_gf256_engine_create(int device, ntc_gf256_engine** out);
 void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
 
 /* Region-MAC formulation (tuning and A/B testing; results are identical).  AUTO picks the
- * bit-sliced XOR kernel when the stride fills >= 50 % of its 2 KiB wave span (stride % 32 == 0),
+ * bit-sliced XOR kernel when the stride fills >= 1/3 of its 2 KiB wave span (stride % 16 == 0),
  * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice environment variable overrides
  * AUTO process-wide. */
 enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2 };

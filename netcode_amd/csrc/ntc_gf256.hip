@@ -2143,8 +2143,8 @@ mac_fn pick_kernel(bool dec, int D)
 
 // MAC formulation for a stride.  The bit-sliced kernel spans 2 KiB per wave (two 16-byte pieces per
 // lane), so short symbols leave lanes idle; measured on MI355X it beats the v_perm
-// kernel (8-byte lanes) once >= ~50 % of its lanes carry data (config 2, 1 KiB symbols: 961-979 vs
-// 853-857 GiB/s with the shared-table chain).
+// kernel (8-byte lanes) once >= ~1/3 of its lanes carry data (k=32 r=8, G=8192: 512 B symbols
+// 606 vs 794 GiB/s, 768 B 888 vs 765, 1 KiB 1139 vs 999 -- bit-sliced vs v_perm).
 // NTC_GF256_MAC=perm|bitslice forces one (A/B experiments).
 bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
 {
@@ -2159,7 +2159,7 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
   }();
   if (forced) return forced == 2;
   const uint32_t pieces = stride / 16, spans = (stride + 2047) / 2048;   // 16-B pieces per span: 128
-  return pieces * 100 >= spans * 128 * 50;
+  return pieces * 100 >= spans * 128 * 33;
 }
 
 // The bit-sliced MAC's chain (gf_bitslice_gidx.inc / gf_bitslice_chain.inc).  Default 3: one
@@ -2377,7 +2377,7 @@ const char* ntc_gf256_last_error(void) { return g_err.c_str(); }
 const char* ntc_gf256_build_info(void)
 {
   return "libntc_gf256 gfx950: bit-sliced XOR MAC (32 B lanes, 8-row tiles, one shared 256-block "
-         "table entered per row with VGPR-relative accumulators) for strides filling >= 50 % of a "
+         "table entered per row with VGPR-relative accumulators) for strides filling >= 1/3 of a "
          "2 KiB wave span; v_perm_b32 3/3/2 split MAC (R in {4,8,16,32}, D in {1,2,4}) otherwise";
 }
 

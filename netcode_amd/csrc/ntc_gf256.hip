@@ -2277,6 +2277,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       case 1: fn = gf_mac_bj<8, false, 1, 3>; break;
       case 2: fn = gf_mac_bj<8, false, 2, 3>; break;
       case 3: fn = gf_mac_bj<8, false, 3, 3>; break;
+      case 16: fn = gf_mac_bj<8, false, 16, 3>; break;
       case 64: fn = gf_mac_bj<8, false, 64, 3>; break;
       case 67: fn = gf_mac_bj<8, false, 67, 3>; break;
       default: break;

@@ -167,6 +167,7 @@ struct MacArgs {
   uint32_t ntiles;
   const uint64_t* row_ptr;     // bit-sliced decode: input row address per plan position,
                                // [G][k + kBjRing] (plan_rows; the tail repeats position k-1)
+  uint32_t tile_fast;          // bit-sliced task order: 1 = row tile fastest, 0 = column span fastest
 };
 
 // ---- hand-scheduled scalar loads -------------------------------------------------------------
@@ -755,10 +756,21 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_
   const uint32_t nb = gridDim.x;                       // a multiple of 8 (launch_mac)
   const uint32_t b = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
   uint32_t task = uniform(b * kBjWaves + wave);
-  const uint32_t cc = task % a.ncolchunks;
-  task /= a.ncolchunks;
-  const uint32_t tile = task % a.nrowchunks;
-  const uint32_t g = task / a.nrowchunks;
+  // few generations (dense, G = 1): row tiles fastest, so an XCD owns whole column spans and its
+  // L2 serves each source slice to every row tile; many generations: column spans fastest
+  uint32_t cc, tile;
+  if (a.tile_fast) {
+    tile = task % a.nrowchunks;
+    task /= a.nrowchunks;
+    cc = task % a.ncolchunks;
+    task /= a.ncolchunks;
+  } else {
+    cc = task % a.ncolchunks;
+    task /= a.ncolchunks;
+    tile = task % a.nrowchunks;
+    task /= a.nrowchunks;
+  }
+  const uint32_t g = task;
   if (g >= a.G) return;
   const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
   const uint32_t row0 = tile * RT;
@@ -2300,6 +2312,11 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   }
   a.nrowchunks = (a.rows + rowtile - 1) / rowtile;
   a.ncolchunks = (a.stride + span - 1) / span;
+  static const int order = [] {     // NTC_BJ_ORDER=tile|cc overrides the default (A/B builds)
+    const char* v = std::getenv("NTC_BJ_ORDER");
+    return !v ? -1 : (std::string(v) == "tile" ? 1 : 0);
+  }();
+  a.tile_fast = order >= 0 ? static_cast<uint32_t>(order) : (a.G < 64 ? 1u : 0u);
   const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
   const uint64_t wpb = rowtile <= 16 ? kBjWaves : kWaves;     // bit-sliced : v_perm kernel
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;

@@ -64,6 +64,27 @@ def test_dense_invert_structured(gpu, oracle):
         assert (inv[g] == o_inv).all(), g
 
 
+@pytest.mark.parametrize("n,density", [(256, 0.02), (300, 0.05), (512, 0.01)])
+def test_dense_invert_sparse(gpu, oracle, n, density):
+    """Sparse matrices: the owner wave often has no candidate (fallback election), rows of many
+    waves become pivots out of order; some of these matrices are singular."""
+    import torch
+    from netcode_amd import DenseCode
+    G = 3
+    rng = np.random.default_rng(n)
+    vals = rng.integers(1, 256, (G, n, n), dtype=np.uint8)
+    mats = np.where(rng.random((G, n, n)) < density, vals, 0).astype(np.uint8)
+    for g in range(G):           # a random permutation with non-zero entries keeps most invertible
+        mats[g, np.arange(n), rng.permutation(n)] = rng.integers(1, 256, n, dtype=np.uint8)
+    inv, ok = DenseCode(gpu).invert(_dev(mats, gpu))
+    torch.cuda.synchronize(gpu)
+    inv, ok = inv.cpu().numpy(), ok.cpu().numpy()
+    for g in range(G):
+        o_ok, _, o_inv = oracle.dense_decode(mats[g], np.zeros((n, 16), np.uint8))
+        assert bool(ok[g]) == o_ok, (n, g)
+        assert (inv[g] == o_inv).all(), (n, g)
+
+
 @pytest.mark.parametrize("G,n,k,S", [(3, 40, 40, 1024), (2, 128, 128, 4096), (1, 200, 200, 1504)])
 def test_dense_encode_decode(gpu, oracle, G, n, k, S):
     import torch

@@ -1689,12 +1689,15 @@ constexpr int kPlanWaves = 4;
 
 __constant__ __attribute__((aligned(16))) PermTables d_pinv = make_inv_perm_tables();
 
+// Byte i (runtime) of a register array.  Written as mask arithmetic, not as selects or an
+// indexed access: LLVM turns the select-chain form back into a dynamically indexed array, which
+// it can only keep in scratch memory.
 template <int W>
 __device__ __forceinline__ uint32_t byte_dyn(const uint32_t (&v)[W], uint32_t i)
 {
   uint32_t x = 0;
 #pragma unroll
-  for (int w = 0; w < W; ++w) x = (static_cast<uint32_t>(w) == (i >> 2)) ? v[w] : x;
+  for (int w = 0; w < W; ++w) x |= v[w] & (0u - static_cast<uint32_t>(static_cast<uint32_t>(w) == (i >> 2)));
   return (x >> (8u * (i & 3u))) & 0xFFu;
 }
 
@@ -1702,9 +1705,12 @@ template <int W>
 __device__ __forceinline__ void set_byte_dyn(uint32_t (&v)[W], uint32_t i, uint32_t b)
 {
   const uint32_t sh = 8u * (i & 3u);
+  const uint32_t bm = 0xFFu << sh, bv = (b & 0xFFu) << sh;
 #pragma unroll
-  for (int w = 0; w < W; ++w)
-    if (static_cast<uint32_t>(w) == (i >> 2)) v[w] = (v[w] & ~(0xFFu << sh)) | (b << sh);
+  for (int w = 0; w < W; ++w) {
+    const uint32_t sel = 0u - static_cast<uint32_t>(static_cast<uint32_t>(w) == (i >> 2));
+    v[w] = (v[w] & ~(bm & sel)) | (bv & sel);
+  }
 }
 
 // Gauss-Jordan step for column P (compile-time, so every register index is static): false when
@@ -2029,10 +2035,18 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
           uint32_t acc[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) acc[w] = 0;
-          for (uint32_t q = 0; q < ((a.ablate & 2u) ? 0u : m); ++q) {
-            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q);
+          const uint32_t mq = (a.ablate & 2u) ? 0u : m;
+          // the coefficient table of q+1 is looked up while q's products are formed (its LDS
+          // gather is issued after q's selector loads, so their wait leaves it in flight)
+          uint32_t tn[5] = {0, 0, 0, 0, 0};
+          if (mq) {
+            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, 0);
+            tab(((R1 + Sj) * R1) % 255u + 1u, tn);
+          }
+          for (uint32_t q = 0; q < mq; ++q) {
             uint32_t tc[5];
-            tab(((R1 + Sj) * R1) % 255u + 1u, tc);
+#pragma unroll
+            for (int e = 0; e < 5; ++e) tc[e] = tn[e];
             // column q's selector words: 3 x W dwords, read whole (16-byte broadcast loads;
             // words past m are unused)
             uint32_t sq[3][W];
@@ -2047,6 +2061,10 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             } else {
 #pragma unroll
               for (int e = 0; e < 3 * W; ++e) sq[e / W][e % W] = minvS[q][e / W][e % W];
+            }
+            if (q + 1 < mq) {
+              const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q + 1);
+              tab(((R1 + Sj) * R1) % 255u + 1u, tn);
             }
 #pragma unroll
             for (int w = 0; w < W; ++w)

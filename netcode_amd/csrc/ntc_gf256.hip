@@ -735,6 +735,140 @@ __device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32
   }
 }
 
+// Lean loop of the shared-table MAC for full spans (stride % 2048 == 0, k % 4 == 0; gf_mac_bj
+// GX = 4).  The kernel is bound by instruction supply (rocprofv3: ~47 32-byte instruction fetches
+// per source-tile, of which the chain's 8 blocks take 24), so this form trims the per-source
+// loop instead: the loop is unrolled by the ring depth (slot addresses are immediates / loop-
+// invariant SGPRs, no modulo arithmetic), the DMA uses a scalar row base with one lane offset
+// and the instruction offset for the second KiB (which also offsets the LDS address), and it is
+// issued inside the chain's entry block, sharing that block's M0 save / restore.
+__device__ __forceinline__ void dma_full(const uint8_t* row, uint32_t voff, uint32_t slot)
+{
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\t"
+               "s_mov_b32 m0, %3\n\t"
+               "s_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, %2\n\t"
+               "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(row), "s"(slot) : "memory", "scc");
+}
+
+template <bool DEC>
+__device__ __forceinline__ void mac_tile_bjf(const MacArgs& a, uint32_t g, uint32_t tile,
+                                             uint32_t nrows, uint32_t cc, uint32_t lane,
+                                             uint32_t ring)
+{
+  static_assert(kBjRing == 4, "the unrolled loop assumes a 4-slot ring");
+  const size_t stride = a.stride;
+  const uint32_t k = a.k;
+  const uint32_t voff = cc * 2048u + lane * 16u;       // both KiB of the span lie inside the row
+  const uint32_t rlane = ring + lane * 16u;            // this lane's LDS bytes in slot 0
+  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
+  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBjRing) : nullptr;
+  const uint32_t jstep = a.rp / 4u;
+  const uint32_t* jp = reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * 8u);
+  const uint64_t pmask = a.rp >= 8 ? ~0ull : 0xFFFFFFFFull;
+  auto row_at = [&](uint32_t i) -> const uint8_t* {    // prologue only; a scalar (SGPR) address
+    uint64_t v;
+    if constexpr (DEC) v = const_load<uint64_t>(rowp + i);
+    else v = reinterpret_cast<uint64_t>(base0 + (i < k ? i : k - 1) * stride);
+    const uint32_t lo = uniform(static_cast<uint32_t>(v)), hi = uniform(static_cast<uint32_t>(v >> 32));
+    return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  auto lds_row = [&](uint32_t slot, uint32_t (&y)[8]) {
+    const auto* p = reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(rlane + slot * kBjSlot);
+    const u32x4 q0 = p[0], q1 = p[1024 / 16];
+    y[0] = q0[0]; y[1] = q0[1]; y[2] = q0[2]; y[3] = q0[3];
+    y[4] = q1[0]; y[5] = q1[1]; y[6] = q1[2]; y[7] = q1[3];
+  };
+
+  u32x8 A[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tbase;
+  asm volatile("s_getpc_b64 s[96:97]\n"
+               "s_add_u32 s96, s96, ntc_gx3_f@rel32@lo+4\n"
+               "s_addc_u32 s97, s97, ntc_gx3_f@rel32@hi+12\n"
+               "s_add_u32 s98, s96, 32768\n"
+               "s_cbranch_scc0 LT3f%=\n"
+               "s_getpc_b64 s[96:97]\n"
+               "s_add_u32 s96, s96, ntc_gx3_s@rel32@lo+4\n"
+               "s_addc_u32 s97, s97, ntc_gx3_s@rel32@hi+12\n"
+               "LT3f%=:\n"
+               "s_mov_b64 %0, s[96:97]\n"
+               : "=s"(tbase) :: "s96", "s97", "s98", "scc");
+  uint32_t slotm[kBjRing];                             // M0 of each slot (loop-invariant SGPRs)
+#pragma unroll
+  for (int q = 0; q < kBjRing; ++q) slotm[q] = uniform(ring + q * kBjSlot);
+
+#pragma unroll
+  for (int q = 0; q < kBjRing - 1; ++q) dma_full(row_at(q), voff, slotm[q]);
+  const uint8_t* nrow = row_at(kBjRing - 1);           // the refill of iteration 0
+  u32x2 on = const_load<u32x2>(jp);
+  uint32_t ycur[8];
+  vm_wait<2 * (kBjRing - 2)>();
+  lds_row(0, ycur);
+  for (uint32_t i0 = 0; i0 < k; i0 += kBjRing) {
+#pragma unroll
+    for (int u = 0; u < kBjRing; ++u) {
+      const uint32_t i = i0 + u;
+      const u32x2 o = on;
+      uint32_t Y[kBjPlanes];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
+      transpose8(Y);
+      vm_wait<2 * (kBjRing - 3)>();                    // source i+1 has landed
+      lds_row((u + 1) % kBjRing, ycur);
+      jp += (i + 1 < k) ? jstep : 0u;
+      on = const_load<u32x2>(jp);
+      NTC_BJ_TABLES(Y)
+      uint64_t P = ((static_cast<uint64_t>(o[1]) << 32) | o[0]) & pmask;
+      // refill the slot of source i-1 with source i+3, then the chain (one M0 save / restore)
+      asm volatile("s_mov_b32 s94, m0\n"
+                   "s_mov_b32 m0, %[slot]\n"
+                   "s_nop 0\n"
+                   "global_load_lds_dwordx4 %[voff], %[row]\n"
+                   "global_load_lds_dwordx4 %[voff], %[row] offset:1024\n"
+                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+                   "s_lshl_b32 s98, s90, 24\n"
+                   "s_lshr_b32 s98, s98, 17\n"
+                   "s_add_u32 s98, s96, s98\n"
+                   "s_addc_u32 s99, s97, 0\n"
+                   "s_swappc_b64 s[92:93], s[98:99]\n"
+                   "s_set_gpr_idx_off\n"
+                   "s_mov_b32 m0, s94\n"
+                   : NTC_GX_OUTS(A), [p] "+{s[90:91]}"(P)
+                   : NTC_GX3_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slotm[(u + kBjRing - 1) % kBjRing]),
+                     [voff] "v"(voff), [row] "s"(nrow)
+                   : "s92", "s93", "s94", "s98", "s99", "scc", "memory");
+      if constexpr (DEC) nrow = reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i + kBjRing));
+      else nrow += (i + kBjRing < k) ? stride : 0u;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped trailing DMAs
+
+  const uint32_t row0 = tile * 8u;
+  const uint32_t c0 = voff, c1 = voff + 1024u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (static_cast<uint32_t>(j) >= nrows) continue;
+    uint32_t acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = A[j][p];
+    transpose8(acc);
+    uint8_t* dst;
+    if constexpr (DEC) {
+      const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
+      dst = a.out + static_cast<size_t>(g) * k * stride + uniform(outs[j]) * stride;
+    } else {
+      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
+    }
+    *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
 // One wave per (generation, RT-row tile, 2 KiB column span).  Blocks are renumbered so that each
 // XCD (block b runs on XCD b % 8) owns a contiguous range of tasks: the row tiles of one
 // generation then share that XCD's L2 instead of each pulling the sources from HBM.
@@ -784,7 +918,10 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_
       return;
     }
   }
-  if constexpr (GX != 0) {
+  if constexpr (GX == 4) {
+    mac_tile_bjf<DEC>(a, g, tile, nrows, cc, lane, ring);
+    return;
+  } else if constexpr (GX != 0) {
     mac_tile_bj<8, RT, DEC, ABL, GX>(a, g, tile, nrows, cc, lane, ring_p, ring);
     return;
   }
@@ -2335,6 +2472,15 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     return !v ? -1 : (std::string(v) == "tile" ? 1 : 0);
   }();
   a.tile_fast = order >= 0 ? static_cast<uint32_t>(order) : (a.G < 64 ? 1u : 0u);
+  // full 2 KiB spans and k % 4 == 0: the lean-loop form of the shared-table MAC
+  static const bool lean = [] {      // NTC_BJ_FULL=0 keeps the general loop (A/B builds)
+    const char* v = std::getenv("NTC_BJ_FULL");
+    return !v || std::atoi(v) != 0;
+  }();
+  if (lean && a.stride % 2048 == 0 && a.k % 4 == 0 && a.k >= 4) {
+    if (fn == gf_mac_bj<8, false, 0, 3>) fn = gf_mac_bj<8, false, 0, 4>;
+    if (fn == gf_mac_bj<8, true, 0, 3>) fn = gf_mac_bj<8, true, 0, 4>;
+  }
   const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
   const uint64_t wpb = rowtile <= 16 ? kBjWaves : kWaves;     // bit-sliced : v_perm kernel
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;

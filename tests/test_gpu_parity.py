@@ -91,6 +91,9 @@ ENCODE_CASES = [
     (2, 7, 3, 4096, 4112, True, "offset"),            # stride not a multiple of the wave span
     (5, 9, 12, 2080, 2080, True, "offset"),           # 2 KiB spans + a 1-lane tail; 8+4 row tiles
     (6, 21, 20, 2048, 2048, False, "offset"),         # 3 row tiles: plane-sharing group, one idle wave
+    # lean-loop MAC (full 2 KiB spans, k % 4 == 0): only the final group of 4 sources; 3 spans
+    (5, 4, 3, 2048, 2048, True, "offset"),
+    (3, 12, 9, 6144, 6144, True, "wrap"),
 ]
 
 
@@ -145,6 +148,8 @@ DECODE_CASES = [
     (9, 33, 12, 2080, 2080, "exact", 12, True),       # odd k (unaligned plan rows), 8+4 row tiles
     (30, 7, 5, 4096, 4096, "iid", 0.3, False),        # tiny k, mixed outcomes
     (12, 45, 24, 2048, 2048, "mixed", 24, False),     # k % 4 != 0, 1-3 row tiles per generation
+    (20, 8, 8, 2048, 2048, "iid", 0.3, True),         # lean-loop MAC: k = 8 (two groups of 4)
+    (7, 12, 16, 6144, 6144, "exact", 9, False),       # lean-loop MAC: 3 spans, 8+1 row tiles
     # iid loss of sources and repairs, r > 32: a few generations decode only after the first
     # candidate repair fails (decoder.cc:448-468 retry; the LDS plan's rank screening)
     (400, 100, 64, 64, 64, "iid", 0.35, False),

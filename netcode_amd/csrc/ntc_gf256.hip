@@ -1946,10 +1946,28 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 
+  // the first two 64-source chunks' masks and lengths, this generation's repair mask and sizes:
+  // independent loads issued together (one memory round trip instead of one per use; k <= 128
+  // covers every generation of configs 1-4)
+  uint32_t smv[2], slv[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t idx = 64u * c + lane;
+    smv[c] = idx < k ? smask[idx] : 1u;
+    slv[c] = idx < k ? a.src_len[static_cast<size_t>(g) * k + idx] : 0u;
+  }
+  const uint32_t rmv = lane < r ? rmask[lane] : 0u;
+  const uint32_t rsv = lane < r ? a.rep_size[static_cast<size_t>(g) * r + lane] : 0u;
+  auto mask_at = [&](uint32_t base) -> uint32_t {      // smask of source base + lane (or 1 past k)
+    const uint32_t idx = base + lane;
+    if (base == 0) return smv[0];
+    if (base == 64) return smv[1];
+    return idx < k ? smask[idx] : 1u;
+  };
   uint32_t m = 0;
   for (uint32_t base = 0; base < k; base += 64) {
     const uint32_t idx = base + lane;
-    const bool lost = idx < k && smask[idx] == 0;
+    const bool lost = idx < k && mask_at(base) == 0;
     const uint64_t b = __ballot(lost);
     if (lost) {
       const uint32_t pos = m + __popcll(b & lt);
@@ -1959,7 +1977,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   }
   uint32_t nrecv = 0;
   {
-    const bool got = lane < r && rmask[lane] != 0;      // r <= RM <= 32
+    const bool got = lane < r && rmv != 0;              // r <= RM <= 32
     const uint64_t b = __ballot(got);
     if (got) recv[__popcll(b & lt)] = static_cast<uint16_t>(lane);
     nrecv = __popcll(b);
@@ -2141,10 +2159,14 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       // R1 of the repair in row q (rows 0 .. m-2: received repairs 0 .. m-2; row m-1: repair t)
       const uint32_t t_rid1 = __builtin_amdgcn_readlane(rid1, t);
       const uint32_t row_r1 = (lane == m - 1) ? t_rid1 : rid1;
-      // Positions 0 .. m-1: the chosen repairs, D[s][q] = Minv[s][q] = column m + q
-      if (lane >= m && lane < 2 * m) {
+      // Positions 0 .. m-1: the chosen repairs, D[s][q] = Minv[s][q] = column m + q; the size of
+      // each lane's repair from the preloaded sizes (shuffled with every lane active)
+      const bool rep_lane = lane >= m && lane < 2 * m;
+      const uint32_t rq_l = rep_lane ? ((lane - m + 1 < m) ? recv[lane - m] : recv[t]) : 0u;
+      const uint32_t rsz_l = __shfl(rsv, rq_l);
+      if (rep_lane) {
         const uint32_t q = lane - m;
-        const uint32_t rq = (q + 1 < m) ? recv[q] : recv[t];
+        const uint32_t rq = rq_l;
         pin[q] = static_cast<uint16_t>(k + rq);
         put_row(q, a.rows_rep + (static_cast<uint64_t>(g) * r + rq) * a.rows_stride);
         emit(q, col);
@@ -2154,7 +2176,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
           minvS[q][1][w] = (col[w] >> 3) & 0x07070707u;
           minvS[q][2][w] = (col[w] >> 6) & 0x03030303u;
         }
-        size_terms(a.rep_size[static_cast<size_t>(g) * r + rq], col);
+        size_terms(rsz_l, col);
       }
       if (lane < rp) pout[lane] = lane < m ? miss[lane] : 0;
       wave_sync();
@@ -2162,7 +2184,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       uint32_t pos_base = m;
       for (uint32_t base = 0; base < k; base += 64) {
         const uint32_t j = base + lane;
-        const bool got = j < k && smask[j] != 0;
+        const bool got = j < k && mask_at(base) != 0;
+        const uint32_t len_j = base == 0 ? slv[0] : base == 64 ? slv[1] : (got ? slen[j] : 0u);
         const uint64_t b = __ballot(got);
         if (got) {
           const uint32_t pos = pos_base + __popcll(b & lt);
@@ -2211,7 +2234,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
                                __builtin_amdgcn_perm(tc[4], tc[4], sq[2][w]));
           }
           emit(pos, acc);
-          size_terms(slen[j], acc);
+          size_terms(len_j, acc);
         }
         pos_base += __popcll(b);
       }

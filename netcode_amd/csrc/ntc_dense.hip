@@ -89,6 +89,8 @@ struct PanelArgs {
   uint8_t* flag;       // [G][np] 1 = not yet a pivot row (eligible)
   uint8_t* keep;       // [G][np] 0 = chosen as a pivot in this panel
   uint8_t* ok;         // [G] 0 once singular
+  uint32_t ablate;     // NTC_DENSE_ABLATE timing ablations of dn_panel_ra (results are wrong):
+                       // 1 = the other waves skip the records, 2 = the owner skips its own rows
 };
 
 // One workgroup per generation, thread i = row i.  v[0..7]: the row's 32 panel bytes; v[8..15]:
@@ -368,6 +370,165 @@ __global__ __launch_bounds__(1024) void dn_panel_own(PanelArgs a)
   }
 }
 
+// dn_panel with a run-ahead owner wave (the default): pivot order does not change the inverse, so
+// the owner -- one wave that has a candidate -- eliminates the panel's columns on its own 64 rows
+// for as many steps as it keeps finding candidates, writing one record per step (the normalised
+// window with its v_perm selectors) and never waiting on the other waves.  One barrier later the
+// other 15 waves apply every record in step order to their rows.  Only when the owner runs out of
+// candidates at some column is there an election: every wave reports whether it has one, the
+// lowest such wave becomes the next owner (none: singular).  A random dense matrix needs about one
+// phase per panel, i.e. two barriers per 32 pivots instead of 32.
+__global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
+{
+  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];   // tables of c
+  __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
+  __shared__ __attribute__((aligned(16))) u32x4 rec[kPanel][9];      // step records
+  __shared__ uint32_t stopv[2];                                      // owner's stop step per phase
+  __shared__ uint32_t cm[2];                                         // election masks per phase
+  __shared__ uint32_t ne[16];                                        // wave has eligible rows
+
+  const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
+  const uint32_t np = a.np, P = 2 * np;
+  const bool row_ok = i < np;
+  const size_t gi = static_cast<size_t>(g) * np + i;
+  bool elig = row_ok && a.flag[gi] != 0;
+  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) {
+    perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+    pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
+  }
+  if (i < 2) cm[i] = 0;
+  {
+    const uint64_t e0 = __ballot(elig);
+    if (lane == 0) ne[w] = e0 != 0 ? 1u : 0u;
+  }
+  const bool live = a.ok[g] != 0;
+  __syncthreads();
+  if (!live) return;                                   // uniform: a singular generation stops
+  uint32_t owner = 0;
+  for (uint32_t q = blockDim.x / 64u; q-- > 0;) owner = ne[q] ? q : owner;
+  owner = __builtin_amdgcn_readfirstlane(owner);
+
+  uint32_t v[16];
+  if (row_ok) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
+    const u32x4 q0 = src[0], q1 = src[1];
+    v[0] = q0[0]; v[1] = q0[1]; v[2] = q0[2]; v[3] = q0[3];
+    v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
+  } else {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) v[d] = 0;
+  }
+#pragma unroll
+  for (int d = 8; d < 16; ++d) v[d] = 0;
+  bool chosen = false;
+  bool singular = false;
+
+  // row -= f * record s (window of step s), or become record s when this row is its pivot
+  auto apply = [&](int s, bool pivot) {
+    const int q = s >> 2, sh = 8 * (s & 3);
+    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
+    const uint32_t f = (v[q] >> sh) & 0xFFu;
+    if (pivot) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) v[wd(e)] = rec[s][e][0];
+    } else if (f != 0) {
+      const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);
+      const uint32_t tf4 = perm_t[f][4];
+#pragma unroll
+      for (int e = 0; e < 9; ++e) {
+        const u32x4 c4 = rec[s][e];
+        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                               __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
+                   __builtin_amdgcn_perm(tf4, tf4, c4[3]);
+      }
+    }
+  };
+
+  uint32_t t = 0;
+  for (uint32_t phase = 0;; ++phase) {
+    const uint32_t par = phase & 1u;
+    if (w == owner) {                                    // wave-uniform: run ahead from step t
+      uint32_t stop = kPanel;
+#pragma unroll
+      for (int s = 0; s < static_cast<int>(kPanel); ++s) {
+        if (s < static_cast<int>(t)) continue;
+        const int q = s >> 2, sh = 8 * (s & 3);
+        auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
+        const uint32_t f = (v[q] >> sh) & 0xFFu;
+        const uint64_t b = __ballot(elig && f != 0);
+        if (b == 0) { stop = s; break; }
+        const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
+        uint32_t x = 0;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) {
+          uint32_t val = __builtin_amdgcn_readlane(v[wd(e)], first);
+          if (wd(e) == 8 + q) val ^= 1u << sh;
+          x = lane == static_cast<uint32_t>(e) ? val : x;
+        }
+        const uint32_t fc = __builtin_amdgcn_readlane(f, first);
+        const u32x4 ti = *reinterpret_cast<const u32x4*>(&pinv_t[fc][0]);
+        const uint32_t ti4 = pinv_t[fc][4];
+        if (lane < 9) {
+          const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
+          u32x4 o;
+          o[0] = nv;
+          o[1] = nv & 0x07070707u;
+          o[2] = (nv >> 3) & 0x07070707u;
+          o[3] = (nv >> 6) & 0x03030303u;
+          rec[s][lane] = o;
+        }
+        __builtin_amdgcn_wave_barrier();                 // this wave's record writes before its reads
+        const uint32_t prow = w * 64u + first;
+        if (lane == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + s] = prow;
+        const bool me = lane == first;
+        if (!(a.ablate & 2u)) apply(s, me);
+        if (me) { chosen = true; elig = false; }
+      }
+      if (lane == 0) stopv[par] = stop;
+    }
+    __syncthreads();
+    const uint32_t stop = __builtin_amdgcn_readfirstlane(stopv[par]);
+    // the other waves need the records only to elect (phase incomplete) or to finish rows they
+    // gave as pivots in an earlier phase; the trackers of non-pivot rows come from dn_update
+    const bool need = stop < kPanel || __ballot(chosen) != 0;
+    if (w != owner && need && !(a.ablate & 1u)) {
+#pragma unroll
+      for (int s = 0; s < static_cast<int>(kPanel); ++s)
+        if (s >= static_cast<int>(t) && s < static_cast<int>(stop)) apply(s, false);
+    }
+    t = stop;
+    if (t >= kPanel) break;
+    // election at column t: the lowest wave with a candidate owns the next phase
+    uint32_t f = 0;
+#pragma unroll
+    for (int s = 0; s < static_cast<int>(kPanel); ++s)
+      if (s == static_cast<int>(t)) f = (v[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+    const uint64_t b = __ballot(elig && f != 0);
+    if (b != 0 && lane == 0) atomicOr(&cm[par], 1u << w);
+    __syncthreads();
+    const uint32_t m = __builtin_amdgcn_readfirstlane(cm[par]);
+    if (i == 0) cm[par ^ 1u] = 0;                        // next read after two more barriers
+    if (m == 0) { singular = true; break; }              // uniform
+    owner = __ffs(m) - 1;
+  }
+  if (singular) {
+    if (i == 0) a.ok[g] = 0;
+    return;
+  }
+  if (row_ok) {
+    a.flag[gi] = elig ? 1 : 0;
+    a.keep[gi] = chosen ? 0 : 1;
+  }
+  if (chosen) {                                        // T: the pivot rows' trackers only
+    u32x4* wg = reinterpret_cast<u32x4*>(a.W + gi * kPanel);
+    u32x4 o0, o1;
+    o0[0] = v[8]; o0[1] = v[9]; o0[2] = v[10]; o0[3] = v[11];
+    o1[0] = v[12]; o1[1] = v[13]; o1[2] = v[14]; o1[3] = v[15];
+    wg[0] = o0;
+    wg[1] = o1;
+  }
+}
+
 struct UpdArgs {
   uint32_t G, np, c0, cs;      // cs: first column to produce
   uint32_t ntiles, nspans;
@@ -387,6 +548,7 @@ struct UpdArgs {
 __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
 {
   __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
+  __shared__ __attribute__((aligned(16))) uint32_t tT_all[4][kPanel * 8];   // per wave: T by step
   for (uint32_t e = threadIdx.x; e < 256 * 8; e += 256) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
@@ -405,11 +567,40 @@ __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
   uint8_t* Yg = a.Y + static_cast<size_t>(g) * np * P;
   const uint32_t i0 = tile * kUpdRows;
   const uint32_t* piv = a.piv + static_cast<size_t>(g) * np + a.c0;
-  // the tile's 4 x 32 tracker bytes: byte t of row j = word 8j + t/4, all in SGPRs up front
-  const u32x16 w0 = const_load<u32x16>(a.W + (static_cast<size_t>(g) * np + i0) * kPanel);
-  const u32x16 w1 = const_load<u32x16>(a.W + (static_cast<size_t>(g) * np + i0) * kPanel + 64);
-
   const uint32_t kw = const_load<uint32_t>(a.keep + static_cast<size_t>(g) * np + i0);
+  // The tile's 4 x 32 tracker bytes, byte t of row j = word 8j + t/4, moved to SGPRs.  A pivot
+  // row's tracker is the panel's (its row of T = B^-1, B = the pivot rows' panel columns); any
+  // other row's is derived here, not by the panel: its panel columns vanish, so
+  // W_i = X_i[c0 .. c0 + 32) * T -- 32 products per tracker dword, lane 8j + d holding dword d of
+  // row j, T staged in this wave's LDS slice.
+  uint32_t wv[4 * kUpdRows * 2];
+  {
+    uint32_t* tT = tT_all[threadIdx.x >> 6];
+    {
+      const uint32_t s = lane >> 1, h = lane & 1u;
+      const u32x4 q = *reinterpret_cast<const u32x4*>(
+          a.W + (static_cast<size_t>(g) * np + piv[s]) * kPanel + 16u * h);
+      *reinterpret_cast<u32x4*>(&tT[8 * s + 4 * h]) = q;
+    }
+    const uint32_t j = (lane >> 3) & 3u, d = lane & 7u;
+    const u32x4* xr = reinterpret_cast<const u32x4*>(a.X + (static_cast<size_t>(g) * np + i0 + j) * P + a.c0);
+    const u32x4 x0 = xr[0], x1 = xr[1];
+    const uint32_t xw[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    __builtin_amdgcn_wave_barrier();
+    uint32_t acc_w = 0;
+#pragma unroll
+    for (int s = 0; s < static_cast<int>(kPanel); ++s) {
+      const uint32_t c = (xw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+      const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
+      const uint32_t t4 = perm_t[c][4];
+      acc_w ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, tT[8 * s + d]);
+    }
+    if (((kw >> (8 * j)) & 0xFFu) == 0)
+      acc_w = *reinterpret_cast<const uint32_t*>(a.W + (static_cast<size_t>(g) * np + i0 + j) * kPanel + 4u * d);
+#pragma unroll
+    for (int q = 0; q < 4 * kUpdRows * 2; ++q) wv[q] = __builtin_amdgcn_readlane(acc_w, q);
+  }
+
   uint32_t acc[kUpdRows];
 #pragma unroll
   for (int j = 0; j < kUpdRows; ++j)
@@ -436,7 +627,7 @@ __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
 #pragma unroll
       for (int j = 0; j < kUpdRows; ++j) {
         const uint32_t wi = 8u * j + (t >> 2);
-        const uint32_t c = ((wi < 16 ? w0[wi & 15] : w1[wi & 15]) >> (8 * (t & 3))) & 0xFFu;   // 0: zero table
+        const uint32_t c = (wv[wi] >> (8 * (t & 3))) & 0xFFu;   // 0: zero table
         const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
         const uint32_t t4 = perm_t[c][4];
         acc[j] = __builtin_amdgcn_bitop3_b32(acc[j], __builtin_amdgcn_perm(tab[1], tab[0], sa),
@@ -518,13 +709,21 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
   hipLaunchKernelGGL(dn_init, dim3(np, G), dim3(256), 0, st, mat, n, np, X, flag, ok);
   if ((rc = hip_check(hipGetLastError(), "dn_init launch"))) return rc;
   const uint32_t threads = (np + 63) / 64 * 64;
-  static const bool panel_all = [] {     // NTC_DENSE_PANEL=all: every wave elects (A/B builds)
+  // NTC_DENSE_PANEL=all: every wave elects at every step; =own: owner wave, one barrier per step
+  // (A/B builds); default: the run-ahead owner
+  static void (*const panel_kernel)(PanelArgs) = [] {
     const char* v = std::getenv("NTC_DENSE_PANEL");
-    return v && std::string(v) == "all";
+    if (v && std::string(v) == "all") return &dn_panel;
+    if (v && std::string(v) == "own") return &dn_panel_own;
+    return &dn_panel_ra;
+  }();
+  static const uint32_t ablate = [] {
+    const char* v = std::getenv("NTC_DENSE_ABLATE");
+    return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
   for (uint32_t c0 = 0; c0 < np; c0 += kPanel) {
-    PanelArgs pa{np, c0, X, static_cast<uint8_t*>(e->dn_w), static_cast<uint32_t*>(e->dn_piv), flag, keep, ok};
-    hipLaunchKernelGGL(panel_all ? dn_panel : dn_panel_own, dim3(G), dim3(threads), 0, st, pa);
+    PanelArgs pa{np, c0, X, static_cast<uint8_t*>(e->dn_w), static_cast<uint32_t*>(e->dn_piv), flag, keep, ok, ablate};
+    hipLaunchKernelGGL(panel_kernel, dim3(G), dim3(threads), 0, st, pa);
     if ((rc = hip_check(hipGetLastError(), "dn_panel launch"))) return rc;
     UpdArgs ua{};
     ua.G = G; ua.np = np; ua.c0 = c0;

@@ -18,6 +18,8 @@
 //              with keep_i = 0 for the 32 rows chosen as pivots in this panel.
 //   dn_update  applies that to the columns right of the panel (and the identity half) as a
 //              GF(2^8) multiply-accumulate, X -> Y (ping-pong: pivot rows are read by every row).
+// The default panel kernel is dn_panel_ra (run-ahead owner wave, no barrier per step); it leaves
+// the trackers of non-pivot rows to dn_update, which derives them as W_i = X_i[panel] * T.
 // Pivoting takes the lowest-index eligible row with a non-zero entry; the inverse is unique, so
 // the result is the reference's M^-1 whatever the pivot order, and singularity is a rank property.
 #include <hip/hip_runtime.h>

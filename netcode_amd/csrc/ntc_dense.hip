@@ -445,6 +445,20 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
       }
     }
   };
+  // the owner's form: the row's table tf (of its column-s byte) was fetched at the start of the
+  // step, before the record exists, and the pivot row takes the record by a select, not a branch
+  auto apply_own = [&](int s, bool pivot, const u32x4 tf, uint32_t tf4) {
+    const int q = s >> 2;
+    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const u32x4 c4 = rec[s][e];
+      const uint32_t upd = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                                       __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
+                           __builtin_amdgcn_perm(tf4, tf4, c4[3]);
+      v[wd(e)] = pivot ? c4[0] : upd;
+    }
+  };
 
   uint32_t t = 0;
   for (uint32_t phase = 0;; ++phase) {
@@ -457,6 +471,8 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         const int q = s >> 2, sh = 8 * (s & 3);
         auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
         const uint32_t f = (v[q] >> sh) & 0xFFu;
+        const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);   // f = 0: all-zero table
+        const uint32_t tf4 = perm_t[f][4];
         const uint64_t b = __ballot(elig && f != 0);
         if (b == 0) { stop = s; break; }
         const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
@@ -483,7 +499,7 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         const uint32_t prow = w * 64u + first;
         if (lane == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + s] = prow;
         const bool me = lane == first;
-        if (!(a.ablate & 2u)) apply(s, me);
+        if (!(a.ablate & 2u)) apply_own(s, me, tf, tf4);
         if (me) { chosen = true; elig = false; }
       }
       if (lane == 0) stopv[par] = stop;

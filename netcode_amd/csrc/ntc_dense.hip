@@ -473,6 +473,10 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         const uint32_t f = (v[q] >> sh) & 0xFFu;
         const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);   // f = 0: all-zero table
         const uint32_t tf4 = perm_t[f][4];
+        // every row's 1/f table too: the pivot's is then read from its lane (readlane), not
+        // looked up after the pivot is known
+        const u32x4 tl = *reinterpret_cast<const u32x4*>(&pinv_t[f][0]);
+        const uint32_t tl4 = pinv_t[f][4];
         const uint64_t b = __ballot(elig && f != 0);
         if (b == 0) { stop = s; break; }
         const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
@@ -483,9 +487,12 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
           if (wd(e) == 8 + q) val ^= 1u << sh;
           x = lane == static_cast<uint32_t>(e) ? val : x;
         }
-        const uint32_t fc = __builtin_amdgcn_readlane(f, first);
-        const u32x4 ti = *reinterpret_cast<const u32x4*>(&pinv_t[fc][0]);
-        const uint32_t ti4 = pinv_t[fc][4];
+        u32x4 ti;
+        ti[0] = __builtin_amdgcn_readlane(tl[0], first);
+        ti[1] = __builtin_amdgcn_readlane(tl[1], first);
+        ti[2] = __builtin_amdgcn_readlane(tl[2], first);
+        ti[3] = __builtin_amdgcn_readlane(tl[3], first);
+        const uint32_t ti4 = __builtin_amdgcn_readlane(tl4, first);
         if (lane < 9) {
           const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
           u32x4 o;

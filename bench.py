@@ -48,6 +48,17 @@ HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # CUs x SIMDs x lanes/clk x 2.4 GHz
 
 
+def metric_name(config, k, r, S):
+    """BASELINE.json's metric string for its headline config (config 3), the same wording with
+    the workload's own shape for the others."""
+    if config == "k128r32s4096":
+        return "device-resident GF(256) encode+decode GiB/s, k=128 r=32, 4 KiB pkts, 1/2/4/8 GPU"
+    if config == "k1024dense":
+        return f"device-resident GF(256) dense encode+decode GiB/s, k={k} (all lost), {S // 1024} KiB pkts"
+    size = f"{S // 1024} KiB" if S % 1024 == 0 else f"{S} B"
+    return f"device-resident GF(256) encode+decode GiB/s, k={k} r={r}, {size} pkts, 1/2/4/8 GPU"
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -588,6 +599,8 @@ def main():
         dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # physical devices in use: ranks of a gloo test share devices round-robin
+    n_gpus = min(world, ndev) if (backend == "gloo" and ndev) else world
     k, r, S, stride, m, Gdef = CONFIGS[a.config]
     if a.S:
         S, stride = a.S, (a.S + 15) // 16 * 16
@@ -616,23 +629,10 @@ def main():
     # kernels bracketed by events inside the timed steps: the MACs (plus, for the dense config,
     # its two inversion/layout launches: 4 ms steps make the event cost negligible)
     timed_kinds = ("encode_mac", "decode_mac") + (("dense",) if dense else ())
-    # the last nb warmup steps run with every kernel bracketed by events (kernels_ms breakdown);
-    # the timed steps then log only the MAC kernels (roofline), in the same log
-    nb = min(a.warmup, 10)
-    for i in range(a.warmup):
-        if i == a.warmup - nb:
-            torch.cuda.synchronize(dev)
-            engine.timing_log((nb + a.steps) * 16)
-            tb = time.perf_counter()
+    for _ in range(a.warmup):
         w.step()
     torch.cuda.synchronize(dev)
-    if nb:
-        ms_logged = (time.perf_counter() - tb) / nb * 1e3
-        n_breakdown = len(engine.timing_read())
-        engine.timing_kinds(timed_kinds)
-    else:
-        ms_logged, n_breakdown = 0.0, 0
-        engine.timing_log(a.steps * 16, kinds=timed_kinds)
+    engine.timing_log(a.steps * 16, kinds=timed_kinds)
 
     def barrier():
         if world > 1:
@@ -648,12 +648,23 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    full_log = engine.timing_read()
+    log = engine.timing_read()
     engine.timing_log(0)
-    log = full_log[n_breakdown:]
     # outputs of the timed steps, checked after the clock stops (warmup runs straight into the
     # timed loop, with no host-side check idling the GPU between them)
     good, ndec, dec_bytes, dec_macs = w.verify()
+    # breakdown of every kernel: nb more steps right after the timed ones (clocks as warm as in
+    # the timed steps), every launch bracketed by an event pair; the MAC kernels of the line come
+    # from the timed steps themselves
+    nb = min(a.steps, 10)
+    engine.timing_log(nb * 16)
+    tb = time.perf_counter()
+    for _ in range(nb):
+        w.step()
+    torch.cuda.synchronize(dev)
+    ms_logged = (time.perf_counter() - tb) / nb * 1e3
+    after_log = engine.timing_read()
+    engine.timing_log(0)
     if world > 1:
         import torch.distributed as dist
         from netcode_amd.shard import max_over_ranks
@@ -663,7 +674,7 @@ def main():
     payload = G * k * S * world
     value = payload / (elapsed / a.steps) / 2**30
     kern_timed, launches = kernel_summary(log, a.steps, dense)
-    kern = kernel_summary(full_log[:n_breakdown], nb, dense)[0] if nb else {}   # logged warmup
+    kern = kernel_summary(after_log, nb, dense)[0]    # every kernel, the logged steps after
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / its mean launch duration
     # over the timed steps.  Encode MAC: read k*S, write r*S per generation; decode MAC: per
@@ -680,7 +691,7 @@ def main():
     traffic, tsrc = pmc_record("pmc_traffic.json", a.config, dom)
     valu, vsrc = pmc_record("pmc_valu.json", a.config, dom)
     # per-step kernel times: the MAC kernels from the timed steps themselves, the others (prep,
-    # plan, row pointers, dense inversion) from the logged warmup steps
+    # plan, row pointers, dense inversion) from the logged steps after them
     kern_step = dict(kern)
     kern_step.update(kern_timed)
     ksum = sum(kern_step.values())
@@ -695,8 +706,9 @@ def main():
             "valu_profile": valu, "valu_profile_source": vsrc,
             "hbm_copy_probe_GBps": probe if probe is not None else hbm_copy_probe(dev)}
 
-    line = {"metric": "device-resident GF(256) encode+decode GiB/s, k=128 r=32, 4 KiB pkts, 1/2/4/8 GPU",
-            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+    line = {"metric": metric_name(a.config, k, r, S),
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": n_gpus, "ranks": world,
+            "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8 (GF(2^8))",
             "data": "synthetic (seeded random payloads, exact-m uniform loss)",
@@ -709,10 +721,11 @@ def main():
             "roofline": roof,
             "kernels_ms": {n: round(v, 4) for n, v in sorted(kern_step.items())},
             "kernels_ms_note": f"per step: {', '.join(sorted(kern_timed))} from the timed steps "
-                               f"(HIP events on every such launch), the other kernels from the "
-                               f"last {nb} warmup steps, run with every launch bracketed",
-            "kernels_ms_warmup_logged": {n: round(v, 4) for n, v in sorted(kern.items())},
-            "ms_per_step_warmup_logged": round(ms_logged, 4),
+                               f"(HIP events on every such launch), the other kernels from "
+                               f"{nb} steps run right after the timed ones with every launch "
+                               f"bracketed",
+            "kernels_ms_after_logged": {n: round(v, 4) for n, v in sorted(kern.items())},
+            "ms_per_step_after_logged": round(ms_logged, 4),
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_step),
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}
@@ -727,7 +740,7 @@ def main():
         line["host_resident_serial_GiBps"] = round(hs, 3)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         _, _, usable = cpu_info()
-        thr = a.cpu_threads or min(16, usable)
+        thr = a.cpu_threads or usable          # every CPU this process may run on
         line["cpu_baseline"] = (cpu_baseline_dense(w) if dense
                                 else cpu_baseline(k, r, S, stride, m, thr))
     if rank == 0:

@@ -81,8 +81,18 @@ CPP_CHECKS = {
     # the detail layer (include/netcode/detail/*.hh)
     "ref_unit_detail": ([REF + "/tests/netcode/detail/" + f for f in (
         "test_buffer.cc", "test_galois_field.cc", "test_square_matrix.cc", "test_source_list.cc",
-        "test_encoder.cc", "test_decoder.cc")] + [REF + "/tests/netcode/test_reconstruction.cc"], True),
+        "test_encoder.cc", "test_decoder.cc", "test_invert_matrix.cc", "test_packetizer.cc")]
+        + [REF + "/tests/netcode/test_reconstruction.cc"], True),
+    # the two suites that need nothing but host code (scalar field ops, detail::invert, the
+    # packetizer): also run by the CPU test suite
+    "ref_unit_host": ([REF + "/tests/netcode/detail/" + f for f in (
+        "test_invert_matrix.cc", "test_packetizer.cc")], True),
 }
+# Boost is absent from the image.  test_invert_matrix.cc includes <boost/optional/optional_io.hpp>
+# (for Catch's printing) and test_packetizer.cc calls boost::endian::native_to_big, which the
+# reference's packetizer.hh brings in; tests/boost_shim holds just those two pieces (nothing under
+# netcode/), on the include path of the reference Catch suites and force-included there.
+BOOST_SHIM = os.path.join(ROOT, "tests", "boost_shim")
 
 
 def _ref_include_dir() -> str:
@@ -121,7 +131,8 @@ def build_cpp_checks(verbose: bool = True) -> list[str]:
             continue
         out = os.path.join(OUT_DIR, name)
         deps = srcs_p + [os.path.join(HERE, "libntc.so"), os.path.abspath(__file__)]
-        for d in ("include/netcode", "include/netcode/detail", "include/netcode/c"):
+        for d in ("include/netcode", "include/netcode/detail", "include/netcode/c",
+                  "tests/boost_shim/boost/optional", "tests/boost_shim/boost/endian"):
             dd = os.path.join(ROOT, d)
             deps += [os.path.join(dd, f) for f in os.listdir(dd)]
         if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps if os.path.exists(d)):
@@ -134,7 +145,8 @@ def build_cpp_checks(verbose: bool = True) -> list[str]:
         if is_ref:
             cmd += ["-I", _ref_include_dir()]
         if catch:
-            cmd += ["-DCATCH_CONFIG_NO_POSIX_SIGNALS", "-I", REF + "/ext"]
+            cmd += ["-DCATCH_CONFIG_NO_POSIX_SIGNALS", "-I", REF + "/ext", "-I", BOOST_SHIM,
+                    "-include", "boost/endian/conversion.hpp"]
         cmd += ["-o", out] + srcs_p
         if catch:
             cmd.append(_catch_main(verbose))

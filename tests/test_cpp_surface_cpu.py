@@ -37,6 +37,18 @@ def test_no_device_fails_loudly(cpp_checks):
     assert "no MI355X engine" in r.stderr
 
 
+@pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="reference tree not present")
+def test_reference_host_suites(cpp_checks):
+    """The reference's tests/netcode/detail/test_invert_matrix.cc (detail::invert equals the
+    embedded jerasure inversion, :123-157; the singular 3x3 fails, :161-180; M * M^-1 = I for
+    w = 4/8/16/32, :184-233) and test_packetizer.cc (ack / repair / source round trips, the
+    hand-built truncated packets of :160-229), compiled unmodified against include/ with the
+    tests-only Boost shim (tests/boost_shim); host code only, so they run here."""
+    r = subprocess.run([cpp_checks["ref_unit_host"]], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "All tests passed" in r.stdout, r.stdout[-2000:]
+
+
 def test_detail_packetizer_cases(cpp_checks):
     """The detail-layer packetizer (include/netcode/detail/packetizer.hh) on the cases of the
     reference's test_packetizer.cc (not buildable here: Boost.Endian) plus the SURVEY §8(c) wire

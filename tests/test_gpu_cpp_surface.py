@@ -93,9 +93,16 @@ def test_reference_unit_tests_detail(gpu):
     work on the MI355X engine): test_buffer, test_galois_field (x * 1/x = 1 for w = 4/8/16/32),
     test_square_matrix, test_source_list, detail/test_encoder, detail/test_decoder (reconstruct,
     remove, useless, missing, outdated, 2- and 5-loss full decodings, duplicates, ordering) and
-    test_reconstruction.  Not compiled (they need Boost, absent from the image):
-    test_invert_matrix.cc (boost/optional/optional_io.hpp) and test_packetizer.cc
-    (boost::endian); test_serialize_packet.cc covers the out-of-scope packet dump aid."""
+    test_reconstruction, plus test_invert_matrix.cc (jerasure equality, the singular matrix,
+    M * M^-1 = I) and test_packetizer.cc (hand-built truncated packets), which compile against
+    the tests-only Boost shim (tests/boost_shim: optional_io.hpp, endian::native_to_big).
+    test_serialize_packet.cc covers the out-of-scope packet dump aid."""
     r = _run("ref_unit_detail", timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "All tests passed" in r.stdout, r.stdout[-2000:]
+    # the two suites added with the Boost shim ran inside this binary: list its test cases
+    names = subprocess.run([os.path.join(BUILD, "ref_unit_detail"), "--list-test-names-only"],
+                           capture_output=True, text=True, timeout=60).stdout
+    for case in ("Compare with jerasure matrix inversion", "Non-invertible matrix",
+                 "Matrix is correctly inverted", "Prevent buffer overflow"):
+        assert case in names, case

@@ -97,7 +97,7 @@ int  ntc_gf256_mac_time(ntc_gf256_engine* eng, int dec, float* ms);
  * `mask` (default: all): every logged kernel costs two event records on its stream, a few
  * microseconds that matter for sub-millisecond steps. */
 enum { NTC_GF256_K_ENCODE_PREP = 0, NTC_GF256_K_ENCODE_MAC = 1, NTC_GF256_K_DECODE_PLAN = 2,
-       NTC_GF256_K_PLAN_ROWS = 3, NTC_GF256_K_DECODE_MAC = 4, NTC_GF256_K_BJ_OFFSETS = 5,
+       NTC_GF256_K_PLAN_ROWS = 3, NTC_GF256_K_DECODE_MAC = 4, NTC_GF256_K_BJ_OFFSETS = 5 /* reserved */,
        NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 };
 int  ntc_gf256_timing_log(ntc_gf256_engine* eng, uint32_t capacity);
 int  ntc_gf256_timing_kinds(ntc_gf256_engine* eng, uint32_t mask);

@@ -20,11 +20,6 @@ struct ntc_gf256_engine {
   uint8_t* plan_coef = nullptr;
   void* enc_coef = nullptr;
   size_t enc_coef_cap = 0;
-  void* joff = nullptr;        // bit-sliced MAC block offsets (encode; decode via bj_offsets)
-  size_t joff_cap = 0;
-  void* joff_dec = nullptr;    // decode offsets written by decode_plan (ntc_gf256_decode_batch)
-  size_t joff_dec_cap = 0;
-  bool last_plan_offsets = false;
   // the last plan also wrote the decode MAC's input row addresses (row_ptr) for these buffers
   const uint8_t* rows_src = nullptr;
   const uint8_t* rows_rep = nullptr;

@@ -91,288 +91,9 @@ struct PanelArgs {
   uint8_t* flag;       // [G][np] 1 = not yet a pivot row (eligible)
   uint8_t* keep;       // [G][np] 0 = chosen as a pivot in this panel
   uint8_t* ok;         // [G] 0 once singular
-  uint32_t ablate;     // NTC_DENSE_ABLATE timing ablations of dn_panel_ra (results are wrong):
-                       // 1 = the other waves skip the records, 2 = the owner skips its own rows
 };
 
-// One workgroup per generation, thread i = row i.  v[0..7]: the row's 32 panel bytes; v[8..15]:
-// its 32 tracker bytes.  At step t only dwords [t/4, 8) of the panel and [8, 8 + t/4] of the
-// tracker can be non-zero in a candidate row (earlier pivot columns are eliminated, later tracker
-// columns not yet assigned), so every step moves and multiplies exactly 9 dwords.
-// Step t: every wave with a candidate (eligible, non-zero in column t) takes its first one,
-// divides that row's window by its pivot value (tracker column t set: the row becomes pivot t) --
-// window dword e on lane e, gathered with readlane + select -- and publishes each dword with its
-// three v_perm selectors.  After the step's one barrier the lowest candidate is the pivot and
-// every other row subtracts f * (published window), f = its own column-t byte, whose table was
-// fetched before the barrier: 3 v_perm + 2 bitwise ops per dword.
-__global__ __launch_bounds__(1024) void dn_panel(PanelArgs a)
-{
-  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];   // tables of c
-  __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
-  __shared__ uint32_t cmask[3];
-  __shared__ uint32_t crow[2][16];
-  __shared__ __attribute__((aligned(16))) u32x4 cbuf[2][16][9];     // {value, sel_a, sel_b, sel_e}
-
-  const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
-  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) {
-    perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
-    pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
-  }
-  if (i < 3) cmask[i] = 0;
-  const bool live = a.ok[g] != 0;
-  __syncthreads();
-  if (!live) return;                                   // uniform: a singular generation stops
-
-  const uint32_t np = a.np, P = 2 * np;
-  const bool row_ok = i < np;
-  const size_t gi = static_cast<size_t>(g) * np + i;
-  uint32_t v[16];
-  if (row_ok) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
-    const u32x4 q0 = src[0], q1 = src[1];
-    v[0] = q0[0]; v[1] = q0[1]; v[2] = q0[2]; v[3] = q0[3];
-    v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
-  } else {
-#pragma unroll
-    for (int d = 0; d < 8; ++d) v[d] = 0;
-  }
-#pragma unroll
-  for (int d = 8; d < 16; ++d) v[d] = 0;
-  bool elig = row_ok && a.flag[gi] != 0;
-  bool chosen = false;
-  bool singular = false;
-
-#pragma unroll
-  for (int t = 0; t < static_cast<int>(kPanel); ++t) {
-    const int q = t >> 2, sh = 8 * (t & 3), par = t & 1;
-    // window entry e -> row dword: panel dwords q..7, then tracker dwords 8..8+q
-    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
-    const uint32_t f = (v[q] >> sh) & 0xFFu;
-    const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);   // f = 0: all-zero table
-    const uint32_t tf4 = perm_t[f][4];
-    const uint64_t b = __ballot(elig && f != 0);
-    if (b != 0) {                                      // wave-uniform
-      const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
-      uint32_t x = 0;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) {
-        uint32_t val = __builtin_amdgcn_readlane(v[wd(e)], first);
-        if (wd(e) == 8 + q) val ^= 1u << sh;
-        x = lane == static_cast<uint32_t>(e) ? val : x;
-      }
-      const uint32_t fc = __builtin_amdgcn_readlane(f, first);
-      const u32x4 ti = *reinterpret_cast<const u32x4*>(&pinv_t[fc][0]);
-      const uint32_t ti4 = pinv_t[fc][4];
-      if (lane < 9) {
-        const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
-        u32x4 o;
-        o[0] = nv;
-        o[1] = nv & 0x07070707u;
-        o[2] = (nv >> 3) & 0x07070707u;
-        o[3] = (nv >> 6) & 0x03030303u;
-        cbuf[par][w][lane] = o;
-      }
-      if (lane == 0) {
-        crow[par][w] = w * 64u + first;
-        atomicOr(&cmask[t % 3], 1u << w);
-      }
-    }
-    __syncthreads();
-    const uint32_t m = cmask[t % 3];
-    if (i == 0) cmask[(t + 2) % 3] = 0;                // next used at step t + 2
-    if (m == 0) { singular = true; break; }            // uniform
-    const uint32_t ws = __ffs(m) - 1;                  // lowest wave = lowest row index
-    const uint32_t prow = crow[par][ws];
-    if (i == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + t] = prow;
-    if (i == prow) {
-      chosen = true;
-      elig = false;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) v[wd(e)] = cbuf[par][ws][e][0];
-    } else if (f != 0) {
-#pragma unroll
-      for (int e = 0; e < 9; ++e) {
-        const u32x4 c4 = cbuf[par][ws][e];
-        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
-                                               __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
-                   __builtin_amdgcn_perm(tf4, tf4, c4[3]);
-      }
-    }
-  }
-  if (singular) {
-    if (i == 0) a.ok[g] = 0;
-    return;
-  }
-  if (row_ok) {
-    a.flag[gi] = elig ? 1 : 0;
-    a.keep[gi] = chosen ? 0 : 1;
-    u32x4* wg = reinterpret_cast<u32x4*>(a.W + gi * kPanel);
-    u32x4 o0, o1;
-    o0[0] = v[8]; o0[1] = v[9]; o0[2] = v[10]; o0[3] = v[11];
-    o1[0] = v[12]; o1[1] = v[13]; o1[2] = v[14]; o1[3] = v[15];
-    wg[0] = o0;
-    wg[1] = o1;
-  }
-}
-
-// dn_panel with an owner wave (the default): the pivot of column t is the lowest eligible row with
-// a non-zero column-t byte, so it lies in the lowest wave that still has eligible rows -- the
-// owner -- unless none of the owner's eligible rows has one.  Every wave tracks the set of waves
-// with eligible rows (it changes only when a pivot empties its wave, which the pivot's record
-// says), so per step only the owner looks for a candidate, normalises it and publishes the
-// window; after the step's barrier the others read one record (one LDS round trip, against
-// cmask -> crow -> cbuf for the all-waves election).  When the owner has no candidate its record
-// says so and the step falls back to that election (a second barrier).  Same pivots, same W.
-__global__ __launch_bounds__(1024) void dn_panel_own(PanelArgs a)
-{
-  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];   // tables of c
-  __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
-  __shared__ uint32_t cmask[3];
-  __shared__ uint32_t crow[2][16];
-  __shared__ __attribute__((aligned(16))) u32x4 cbuf[2][16][9];     // election records
-  __shared__ __attribute__((aligned(16))) u32x4 orec[2][10];        // owner record; [9].x = info
-  __shared__ uint32_t ne[16];                                        // wave has eligible rows
-
-  constexpr uint32_t kOk = 1u << 30, kEmptied = 1u << 31;
-  const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
-  const uint32_t np = a.np, P = 2 * np;
-  const bool row_ok = i < np;
-  const size_t gi = static_cast<size_t>(g) * np + i;
-  bool elig = row_ok && a.flag[gi] != 0;
-  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) {
-    perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
-    pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
-  }
-  if (i < 3) cmask[i] = 0;
-  {
-    const uint64_t e0 = __ballot(elig);
-    if (lane == 0) ne[w] = e0 != 0 ? 1u : 0u;
-  }
-  const bool live = a.ok[g] != 0;
-  __syncthreads();
-  if (!live) return;                                   // uniform: a singular generation stops
-  uint32_t nonempty = 0;
-  for (uint32_t q = 0; q < blockDim.x / 64u; ++q) nonempty |= ne[q] << q;
-  nonempty = __builtin_amdgcn_readfirstlane(nonempty);
-
-  uint32_t v[16];
-  if (row_ok) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
-    const u32x4 q0 = src[0], q1 = src[1];
-    v[0] = q0[0]; v[1] = q0[1]; v[2] = q0[2]; v[3] = q0[3];
-    v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
-  } else {
-#pragma unroll
-    for (int d = 0; d < 8; ++d) v[d] = 0;
-  }
-#pragma unroll
-  for (int d = 8; d < 16; ++d) v[d] = 0;
-  bool chosen = false;
-  bool singular = false;
-
-  // the candidate row `first` of this wave: its window normalised by 1/f, with v_perm selectors,
-  // dword e on lane e (lanes 0..8); returns the value for lanes < 9
-  auto publish = [&](int q, int sh, uint32_t first, u32x4* dst) {
-    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
-    uint32_t x = 0;
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      uint32_t val = __builtin_amdgcn_readlane(v[wd(e)], first);
-      if (wd(e) == 8 + q) val ^= 1u << sh;
-      x = lane == static_cast<uint32_t>(e) ? val : x;
-    }
-    const uint32_t fc = __builtin_amdgcn_readlane((v[q] >> sh) & 0xFFu, first);
-    const u32x4 ti = *reinterpret_cast<const u32x4*>(&pinv_t[fc][0]);
-    const uint32_t ti4 = pinv_t[fc][4];
-    if (lane < 9) {
-      const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
-      u32x4 o;
-      o[0] = nv;
-      o[1] = nv & 0x07070707u;
-      o[2] = (nv >> 3) & 0x07070707u;
-      o[3] = (nv >> 6) & 0x03030303u;
-      dst[lane] = o;
-    }
-  };
-
-#pragma unroll
-  for (int t = 0; t < static_cast<int>(kPanel); ++t) {
-    const int q = t >> 2, sh = 8 * (t & 3), par = t & 1;
-    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
-    const uint32_t f = (v[q] >> sh) & 0xFFu;
-    const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);   // f = 0: all-zero table
-    const uint32_t tf4 = perm_t[f][4];
-    const uint32_t owner = __ffs(nonempty) - 1;          // nonempty != 0 (np - c0 >= 32 rows left)
-    if (w == owner) {                                    // wave-uniform
-      const uint64_t el = __ballot(elig);
-      const uint64_t b = __ballot(elig && f != 0);
-      if (b != 0) {
-        const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
-        publish(q, sh, first, &orec[par][0]);
-        const uint32_t emptied = (el & ~(1ull << first)) == 0 ? kEmptied : 0u;
-        if (lane == 0) orec[par][9][0] = (w * 64u + first) | kOk | emptied;
-      } else if (lane == 0) {
-        orec[par][9][0] = 0;
-      }
-    }
-    __syncthreads();
-    uint32_t info = orec[par][9][0];
-    if (i == 0) cmask[(t + 2) % 3] = 0;                // next used at step t + 2
-    const u32x4* rec = &orec[par][0];
-    if (!(info & kOk)) {                                 // uniform: the all-waves election
-      const uint64_t el = __ballot(elig);
-      const uint64_t b = __ballot(elig && f != 0);
-      if (b != 0) {
-        const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
-        publish(q, sh, first, &cbuf[par][w][0]);
-        if (lane == 0) {
-          crow[par][w] = (w * 64u + first) | ((el & ~(1ull << first)) == 0 ? kEmptied : 0u);
-          atomicOr(&cmask[t % 3], 1u << w);
-        }
-      }
-      __syncthreads();
-      const uint32_t m = cmask[t % 3];
-      if (m == 0) { singular = true; break; }          // uniform
-      const uint32_t ws = __ffs(m) - 1;                // lowest wave = lowest row index
-      info = crow[par][ws];
-      rec = &cbuf[par][ws][0];
-    }
-    info = __builtin_amdgcn_readfirstlane(info);
-    const uint32_t prow = info & 0xFFFFu;
-    if (info & kEmptied) nonempty &= ~(1u << (prow >> 6));
-    if (i == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + t] = prow;
-    if (i == prow) {
-      chosen = true;
-      elig = false;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) v[wd(e)] = rec[e][0];
-    } else if (f != 0) {
-#pragma unroll
-      for (int e = 0; e < 9; ++e) {
-        const u32x4 c4 = rec[e];
-        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
-                                               __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
-                   __builtin_amdgcn_perm(tf4, tf4, c4[3]);
-      }
-    }
-  }
-  if (singular) {
-    if (i == 0) a.ok[g] = 0;
-    return;
-  }
-  if (row_ok) {
-    a.flag[gi] = elig ? 1 : 0;
-    a.keep[gi] = chosen ? 0 : 1;
-    u32x4* wg = reinterpret_cast<u32x4*>(a.W + gi * kPanel);
-    u32x4 o0, o1;
-    o0[0] = v[8]; o0[1] = v[9]; o0[2] = v[10]; o0[3] = v[11];
-    o1[0] = v[12]; o1[1] = v[13]; o1[2] = v[14]; o1[3] = v[15];
-    wg[0] = o0;
-    wg[1] = o1;
-  }
-}
-
-// dn_panel with a run-ahead owner wave (the default): pivot order does not change the inverse, so
+// Panel factorisation with a run-ahead owner wave: pivot order does not change the inverse, so
 // the owner -- one wave that has a candidate -- eliminates the panel's columns on its own 64 rows
 // for as many steps as it keeps finding candidates, writing one record per step (the normalised
 // window with its v_perm selectors) and never waiting on the other waves.  One barrier later the
@@ -506,7 +227,7 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         const uint32_t prow = w * 64u + first;
         if (lane == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + s] = prow;
         const bool me = lane == first;
-        if (!(a.ablate & 2u)) apply_own(s, me, tf, tf4);
+        apply_own(s, me, tf, tf4);
         if (me) { chosen = true; elig = false; }
       }
       if (lane == 0) stopv[par] = stop;
@@ -516,7 +237,7 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
     // the other waves need the records only to elect (phase incomplete) or to finish rows they
     // gave as pivots in an earlier phase; the trackers of non-pivot rows come from dn_update
     const bool need = stop < kPanel || __ballot(chosen) != 0;
-    if (w != owner && need && !(a.ablate & 1u)) {
+    if (w != owner && need) {
 #pragma unroll
       for (int s = 0; s < static_cast<int>(kPanel); ++s)
         if (s >= static_cast<int>(t) && s < static_cast<int>(stop)) apply(s, false);
@@ -734,21 +455,9 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
   hipLaunchKernelGGL(dn_init, dim3(np, G), dim3(256), 0, st, mat, n, np, X, flag, ok);
   if ((rc = hip_check(hipGetLastError(), "dn_init launch"))) return rc;
   const uint32_t threads = (np + 63) / 64 * 64;
-  // NTC_DENSE_PANEL=all: every wave elects at every step; =own: owner wave, one barrier per step
-  // (A/B builds); default: the run-ahead owner
-  static void (*const panel_kernel)(PanelArgs) = [] {
-    const char* v = std::getenv("NTC_DENSE_PANEL");
-    if (v && std::string(v) == "all") return &dn_panel;
-    if (v && std::string(v) == "own") return &dn_panel_own;
-    return &dn_panel_ra;
-  }();
-  static const uint32_t ablate = [] {
-    const char* v = std::getenv("NTC_DENSE_ABLATE");
-    return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
-  }();
   for (uint32_t c0 = 0; c0 < np; c0 += kPanel) {
-    PanelArgs pa{np, c0, X, static_cast<uint8_t*>(e->dn_w), static_cast<uint32_t*>(e->dn_piv), flag, keep, ok, ablate};
-    hipLaunchKernelGGL(panel_kernel, dim3(G), dim3(threads), 0, st, pa);
+    PanelArgs pa{np, c0, X, static_cast<uint8_t*>(e->dn_w), static_cast<uint32_t*>(e->dn_piv), flag, keep, ok};
+    hipLaunchKernelGGL(dn_panel_ra, dim3(G), dim3(threads), 0, st, pa);
     if ((rc = hip_check(hipGetLastError(), "dn_panel launch"))) return rc;
     UpdArgs ua{};
     ua.G = G; ua.np = np; ua.c0 = c0;

@@ -163,10 +163,8 @@ struct MacArgs {
   const uint16_t* out_idx;     // decode: plan_out [G][rp] (destination source slot per row)
   const uint8_t* coef;         // [G][k][rp] coefficient bytes, row-minor
   uint32_t rp;
-  const uint32_t* joff;        // bit-sliced kernel: block offsets [G][k][ntiles][16]
-  uint32_t ntiles;
   const uint64_t* row_ptr;     // bit-sliced decode: input row address per plan position,
-                               // [G][k + kBjRing] (plan_rows; the tail repeats position k-1)
+                               // [G][k + kBsRing] (plan_rows; the tail repeats position k-1)
   uint32_t tile_fast;          // bit-sliced task order: 1 = row tile fastest, 0 = column span fastest
 };
 
@@ -348,27 +346,22 @@ __device__ __forceinline__ void mac_tile(const MacArgs& a, uint32_t g, uint32_t 
   }
 }
 
-// ---- bit-sliced MAC: jump-chained XOR blocks ---------------------------------------------------
-// A lane owns 32 bytes = 8 dwords.  transpose8 turns them into 8 bit-planes (plane p = bit p of
-// every byte; an involution, so the same code slices and un-slices).  Multiplication by c is then
-// linear over GF(2): plane p of c*x is an XOR of input planes.  Per source the XOR combinations
-// of planes 0-3 and of planes 4-7 are built once (Four-Russians tables, 30 planes); each
-// (row, coefficient nibble) "site" is a table of 16 fixed-size blocks of one v_bitop3 per output
-// plane (gf_bitslice_chain.inc, generated by tools/gen_bitslice_chain.py); a source's 2R sites
-// run as a chain of s_setpc jumps whose block offsets bj_offsets precomputed from the coefficient
-// matrix.  Per (source, row) that is 15 full-rate VALU ops for 32 bytes plus 4 scalar ops,
-// against 24 half-rate v_perm + 12 XOR for the byte-domain kernel.
-#include "gf_bitslice_chain.inc"
-// The shared-table variant (one dispatch per row, VGPR-relative accumulators; the GX kernels):
-// tools/gen_bitslice_gidx.py.
-#include "gf_bitslice_gidx.inc"
+// ---- bit-sliced MAC ------------------------------------------------------------------------
+// A lane owns 32 bytes = 8 dwords of a 2 KiB column span.  transpose8 turns them into 8 bit-
+// planes (plane p = bit p of every byte; an involution, so the same code slices and un-slices).
+// Multiplication by c is then linear over GF(2): plane p of c*x is an XOR of input planes.  Per
+// source the XOR combinations of planes 0-3 and of planes 4-7 are built once (Four-Russians
+// tables, 30 planes, NTC_BS_TABLES) and the tile's rows run as a chain of jumps into one shared
+// table of 256 blocks, block c = the <= 8 v_bitop3 of acc ^= c*x on the row selected by VGPR-
+// relative addressing (gf_bitslice_table.inc, tools/gen_bitslice_table.py).
+#include "gf_bitslice_table.inc"
 
-// Variant 3's block table, once per code object: never called (it starts with s_endpgm); the MAC
-// kernels enter it with s_swappc and it returns through s92:93.
-extern "C" __device__ __attribute__((used, noinline)) void ntc_gx3_tables() { asm volatile(NTC_GX3_TABLES); }
+// The block table, once per code object: never called (it starts with s_endpgm); the MAC kernels
+// enter it with s_swappc and it returns through s92:93.
+extern "C" __device__ __attribute__((used, noinline)) void ntc_bs_tables() { asm volatile(NTC_BS_TABLE_ASM); }
 
 // Delta swap of the `mask` bit groups of b with the groups `sh` bits higher in a: two shifts and
-// two bit-field inserts (v_bfi_b32 / v_bitop3), 4 VALU.
+// two bit-field inserts (v_bitop3 select), 4 VALU.
 __device__ __forceinline__ void swap_blocks(uint32_t& a, uint32_t& b, uint32_t sh, uint32_t mask)
 {
   // bitop3 0xCA = S0 ? S1 : S2 (bitwise select)
@@ -391,10 +384,9 @@ __device__ __forceinline__ void transpose8(uint32_t* d)
   for (int i = 0; i < 8; i += 2) swap_blocks(d[i], d[i + 1], 1, 0x55555555u);
 }
 
-typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
-
 // Loads through the constant address space: always scalar (s_load) for a uniform address, with
-// the waits placed by the compiler.  Used for data no kernel in flight writes (offsets, plans).
+// the waits placed by the compiler.  Used for data no kernel in flight writes (coefficients,
+// plans, row addresses).
 template <typename T>
 __device__ __forceinline__ T const_load(const void* p)
 {
@@ -402,47 +394,14 @@ __device__ __forceinline__ T const_load(const void* p)
       reinterpret_cast<uintptr_t>(p));
 }
 
-// Block offsets of one (generation, source, row tile): 2*RT sites = RT rows x 2 nibbles.  A thread
-// writes 4 consecutive sites (2 rows) as one 16-byte store.
-__global__ __launch_bounds__(256) void bj_offsets(const uint8_t* __restrict__ coef, uint32_t rp,
-                                                  uint32_t rt, uint32_t ntiles, uint64_t total4,
-                                                  uint32_t* __restrict__ joff)
-{
-  const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  if (idx >= total4) return;
-  const uint32_t quads = rt / 2u;                     // 4-site groups per tile
-  const uint32_t qd = static_cast<uint32_t>(idx % quads);
-  const uint64_t q = idx / quads;
-  const uint32_t tile = static_cast<uint32_t>(q % ntiles);
-  const uint64_t gk = q / ntiles;
-  const uint32_t j0 = tile * rt + 2u * qd;
-  const uint32_t c0 = j0 < rp ? coef[gk * rp + j0] : 0u;
-  const uint32_t c1 = j0 + 1 < rp ? coef[gk * rp + j0 + 1] : 0u;
-  const uint32_t s0 = 4u * qd * kBjSite;
-  uint4 o;
-  o.x = s0 + kBjVo[c0 & 15u];
-  o.y = s0 + kBjSite + kBjVo[c0 >> 4];
-  o.z = s0 + 2u * kBjSite + kBjVo[c1 & 15u];
-  o.w = s0 + 3u * kBjSite + kBjVo[c1 >> 4];
-  reinterpret_cast<uint4*>(joff)[idx] = o;
-}
-
-// Source staging: every wave streams its sources through a private ring of kBjRing LDS slots with
-// LDS-DMA (global_load_lds_dwordx4), kBjRing-1 sources ahead, so HBM latency hides behind ~3
+// Source staging: every wave streams its sources through a private ring of kBsRing LDS slots with
+// LDS-DMA (global_load_lds_dwordx4), kBsRing-1 sources ahead, so HBM latency hides behind ~3
 // chain iterations without holding VGPRs.  A lane owns two 16-byte pieces of the 2 KiB column
 // span -- bytes [16*lane, +16) and [1024 + 16*lane, +16) -- so each DMA and each store is one
-// contiguous KiB per wave, and a half is valid whenever its 16 bytes lie inside the stride.
-#ifndef NTC_BJ_RING
-#define NTC_BJ_RING 4
-#endif
-constexpr int kBjRing = NTC_BJ_RING;    // tuning builds: -DNTC_BJ_RING=5
-constexpr uint32_t kBjSlot = 2048;
-// NTC_BJ_LATE_READ=1: read source i from its ring slot at the top of iteration i instead of one
-// iteration ahead (8 fewer VGPRs live across the chain; tuning builds).
-#ifndef NTC_BJ_LATE_READ
-#define NTC_BJ_LATE_READ 0
-#endif
-constexpr bool kBjLateRead = NTC_BJ_LATE_READ != 0;
+// contiguous KiB per wave, and a piece is valid whenever its 16 bytes lie inside the stride.
+constexpr int kBsRing = 4;              // LDS slots per wave (the loop is unrolled by it)
+constexpr uint32_t kBsSlot = 2048;      // one source's column span
+constexpr int kBsWaves = 4;             // waves (independent tasks) per workgroup
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p)
 {
@@ -451,407 +410,202 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p)
           reinterpret_cast<uintptr_t>(p))));
 }
 
-// DMA one source's two 16-byte pieces per lane into LDS slot `slot` (wave-uniform byte address).
-// M0 is compiler-reserved: saved and restored inside the statement (cdna_hip_programming.md).
-__device__ __forceinline__ void dma_source(const uint8_t* p0, const uint8_t* p1, uint32_t slot)
-{
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\t"
-               "s_mov_b32 m0, %3\n\t"
-               "s_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, off\n\t"
-               "s_add_u32 m0, %3, 0x400\n\t"
-               "s_nop 0\n\t"
-               "global_load_lds_dwordx4 %2, off\n\t"
-               "s_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(p0), "v"(p1), "s"(slot) : "memory", "scc");
-}
-
 // Wait until at most N of this wave's vector-memory operations (LDS-DMA included) are in flight.
-// The "memory" clobber keeps the compiler's LDS reads of the slot below the wait.
+// The "memory" clobber keeps the LDS reads of the slot below the wait.
 template <int N>
 __device__ __forceinline__ void vm_wait()
 {
   asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory");
 }
 
-// This lane's 32 bytes of a ring slot (ordinary LDS loads: the compiler places the lgkmcnt wait at
-// the first use, one chain iteration later).
-__device__ __forceinline__ void ring_read(const uint8_t* slot, uint32_t lane, uint32_t (&y)[8])
+// The block table's address: the fast copy, or the safe one if the fast copy straddles a 4 GiB
+// boundary.  The table sits anywhere in the code object, so the PC-relative offset is a signed
+// 64-bit quantity, added as low half + high half with carry (s_getpc returns the s_add's address;
+// the lo literal sits 4 bytes after it, the hi literal 12).
+__device__ __forceinline__ uint64_t bs_table_base()
 {
-  const u32x4 q0 = *reinterpret_cast<const u32x4*>(slot + lane * 16u);
-  const u32x4 q1 = *reinterpret_cast<const u32x4*>(slot + 1024u + lane * 16u);
-  y[0] = q0[0]; y[1] = q0[1]; y[2] = q0[2]; y[3] = q0[3];
-  y[4] = q1[0]; y[5] = q1[1]; y[6] = q1[2]; y[7] = q1[3];
+  uint64_t tb;
+  asm volatile("s_getpc_b64 s[96:97]\n"
+               "s_add_u32 s96, s96, ntc_bs_f@rel32@lo+4\n"
+               "s_addc_u32 s97, s97, ntc_bs_f@rel32@hi+12\n"
+               "s_add_u32 s98, s96, %1\n"
+               "s_cbranch_scc0 LBSo%=\n"
+               "s_getpc_b64 s[96:97]\n"
+               "s_add_u32 s96, s96, ntc_bs_s@rel32@lo+4\n"
+               "s_addc_u32 s97, s97, ntc_bs_s@rel32@hi+12\n"
+               "LBSo%=:\n"
+               "s_mov_b64 %0, s[96:97]\n"
+               : "=s"(tb) : "i"(kBsSpan + 64) : "s96", "s97", "s98", "scc");
+  return tb;
 }
 
-// ABL != 0: timing ablations of the encode kernel (NTC_GF256_BJ_ABLATE; results are wrong):
-// 1 no transpose, 2 no plane tables, 4 straight-line stand-in for the chain, 8 no chain,
-// 16 every source uses source 0's jump offsets (scalar-cache-resident), 32 every generation reads
-// generation 0's sources (L2-resident), 64 no source DMAs at all (the ring holds stale bytes).
-// GX: the shared-table chains (gf_bitslice_gidx.inc).  GX = 1: a.joff holds, per (generation,
-// source, 8-row tile), 8 u16 block offsets (kGxOff[c] of the tile's rows) instead of the nibble-
-// site jump offsets.  GX = 2: the chain reads the coefficient bytes a.coef [G][k][rp] directly
-// (8 rows = one u64 per source).  R must be 8 (fewer rows carry c = 0, which the chains skip).
-// Lean entry into the shared table (tuning switch, NTC_GX_LEAN=0 builds the original entry)
-#ifndef NTC_GX_LEAN
-#define NTC_GX_LEAN 1
-#endif
-constexpr bool kGxLean = NTC_GX_LEAN != 0;
+template <int R> struct BsCoef;
+template <> struct BsCoef<8> { using T = u32x2; };
+template <> struct BsCoef<16> { using T = u32x4; };
 
-template <int R, int RT, bool DEC, int ABL = 0, int GX = 0>
-__device__ __forceinline__ void mac_tile_bj(const MacArgs& a, uint32_t g, uint32_t tile,
-                                            uint32_t nrows, uint32_t cc, uint32_t lane,
-                                            const uint8_t* ring_p, uint32_t ring)
+// One wave: rows [tile*R, tile*R + nrows) of generation g over the 2 KiB column span cc.
+//   encode: out[row] = sum_i coef[g][i][row] * in0[g][i]
+//   decode: out[out_idx[row]] = sum_i plan_coef[g][i][row] * (input row i of the plan)
+// R = 8: accumulators v32..v95 (<= 128 VGPRs, 4 waves per SIMD).  R = 16: v32..v159, the
+// source's transpose and plane tables amortised over twice the rows, <= 168 VGPRs (3 waves per
+// SIMD); its source is read from LDS at the top of its own iteration (no register copy of the
+// next one).  FULL: the span lies inside the stride (stride % 2048 == 0), so both pieces come
+// from one lane offset; else each piece has its own, clamped to the span's first bytes when it
+// lies past the stride (loaded, never stored).
+template <int R, bool DEC, bool FULL>
+__device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t tile,
+                                        uint32_t nrows, uint32_t cc, uint32_t lane, uint32_t ring)
 {
-  static_assert(!GX || R == 8, "the shared-table chain works on 8-row tiles");
+  static_assert(R == 8 || R == 16, "8- or 16-row tiles");
+  static_assert(kBsRing == 4, "the unrolled loop assumes a 4-slot ring");
+  constexpr bool kLate = R == 16;
+  using CoefV = typename BsCoef<R>::T;
   const size_t stride = a.stride;
   const uint32_t k = a.k;
-  const uint32_t c0 = cc * 2048u + lane * 16u, c1 = c0 + 1024u;
-  const bool v0 = c0 < stride, v1 = c1 < stride;      // stride % 16 == 0: whole pieces
-  const uint32_t x0 = v0 ? c0 : 0u, x1 = v1 ? c1 : 0u;  // invalid pieces read column 0 (unused)
-  const uint8_t* base0 = a.in0 + static_cast<size_t>((ABL & 32) ? 0u : g) * k * stride;
-  const uint8_t* base1 = DEC ? a.in1 + static_cast<size_t>(g) * a.rows * stride : nullptr;
-  constexpr uint32_t kOffDw = GX == 1 ? 4u : 2u * RT;   // offset dwords per (source, tile)
-  // GX = 2: one source's coefficient row is rp bytes (rp % 4 == 0); the tile's 8 start at 8*tile
-  const uint32_t jstep = GX >= 2 ? a.rp / 4u : a.ntiles * kOffDw;
-  const uint32_t* jrow = GX >= 2
-      ? reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * 8u)
-      : a.joff + (static_cast<size_t>(g) * k * a.ntiles + tile) * kOffDw;
-  constexpr int NJ = R == 16 ? 2 : 1;     // offset vectors per source
-  using OffV = typename std::conditional<GX == 1, u32x4,
-               typename std::conditional<GX >= 2, u32x2, u32x16>::type>::type;
-  const uint64_t pmask = a.rp >= 8 ? ~0ull : 0xFFFFFFFFull;   // rp = 4: bytes 4-7 = next source
-  // Offsets and row addresses are loaded with ordinary uniform loads through the constant address
-  // space (s_load, waits placed by the compiler).  Decode reads each input row's address from the
-  // plan_rows table (padded by kBjRing entries, so the prefetches past position k-1 need no
-  // clamp); encode advances its row and offset pointers by a conditional add per source.  Both
-  // keep the per-source scalar work to a few instructions.
-  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBjRing) : nullptr;
-  auto clampk = [&](uint32_t i) -> uint32_t { return i < k ? i : k - 1; };
-  auto row_at = [&](uint32_t i) -> const uint8_t* {    // prologue only
-    if constexpr (DEC) return reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i));
-    else return base0 + clampk(i) * stride;
-  };
-  (void)base1;
-
-  uint32_t acc[R][8];
-#pragma unroll
-  for (int j = 0; j < R; ++j)
-#pragma unroll
-    for (int p = 0; p < 8; ++p) acc[j][p] = 0;
-  u32x8 A[GX ? R : 1];          // GX: the accumulators as register blocks pinned by the chain
-#pragma unroll
-  for (int j = 0; j < (GX ? R : 1); ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
-  (void)pmask;
-  uint64_t tbase = 0;           // GX = 3: the block table (fast copy, or the safe one if the fast
-  if constexpr (GX == 3) {      // copy straddles a 4 GiB boundary), located once per wave
-    // the table sits anywhere in the code object (before this kernel, typically): the PC-relative
-    // offset is a signed 64-bit quantity, added as low half + high half with carry
-    // (the standard PC-relative pair: s_getpc returns the s_add's address; the lo literal sits
-    // 4 bytes after it, the hi literal 12)
-    asm volatile("s_getpc_b64 s[96:97]\n"
-                 "s_add_u32 s96, s96, ntc_gx3_f@rel32@lo+4\n"
-                 "s_addc_u32 s97, s97, ntc_gx3_f@rel32@hi+12\n"
-                 "s_add_u32 s98, s96, 32768\n"
-                 "s_cbranch_scc0 LT3o%=\n"
-                 "s_getpc_b64 s[96:97]\n"
-                 "s_add_u32 s96, s96, ntc_gx3_s@rel32@lo+4\n"
-                 "s_addc_u32 s97, s97, ntc_gx3_s@rel32@hi+12\n"
-                 "LT3o%=:\n"
-                 "s_mov_b64 %0, s[96:97]\n"
-                 : "=s"(tbase) :: "s96", "s97", "s98", "scc");
-  }
-
-  // Prologue: sources 0 .. kBjRing-2 in flight (indices clamped, so the wait counts are constant);
-  // source 0 read into registers.  Steady state at iteration i: source i in registers, the LDS
-  // read of source i+1 in flight, DMAs of i+2 .. i+kBjRing-1 in flight.
-#pragma unroll
-  for (int q = 0; q < kBjRing - 1; ++q) {
-    const uint8_t* row = row_at(q);
-    if constexpr (!(ABL & 64)) dma_source(row + x0, row + x1, ring + q * kBjSlot);
-  }
-  // row of source i + kBjRing - 1, the refill of iteration i (decode: loaded one iteration ahead)
-  const uint8_t* nrow = row_at(kBjRing - 1);
-  const uint32_t* jp = jrow;                           // offsets of source min(i + 1, k - 1)
-  OffV on[NJ];
-#pragma unroll
-  for (int h = 0; h < NJ; ++h) on[h] = const_load<OffV>(jrow + 16 * h);
-  auto next_offsets = [&](uint32_t i) {
-    if constexpr (!(ABL & 16)) jp += (i + 1 < k) ? jstep : 0u;
-#pragma unroll
-    for (int h = 0; h < NJ; ++h) on[h] = const_load<OffV>(jp + 16 * h);
-  };
-  uint32_t ycur[8];
-  if constexpr (!kBjLateRead) {
-    vm_wait<2 * (kBjRing - 2)>();
-    ring_read(ring_p, lane, ycur);
-  }
-  uint32_t Yk[kBjPlanes];      // ABL & 2 with the shared table: the tables kept from source 0
-  (void)Yk;
-  for (uint32_t i = 0; i < k; ++i) {
-    OffV o[NJ];
-#pragma unroll
-    for (int h = 0; h < NJ; ++h) o[h] = on[h];
-    uint32_t Y[kBjPlanes];
-    if constexpr (kBjLateRead) {
-      // source i's DMA has landed once only those of i+1 .. i+kBjRing-2 remain; read it straight
-      // into the planes (its LDS latency is exposed, hidden by the other waves of the SIMD)
-      vm_wait<2 * (kBjRing - 2)>();
-      ring_read(ring_p + (i % kBjRing) * kBjSlot, lane, ycur);
-    }
-#pragma unroll
-    for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
-    if constexpr (!(ABL & 1)) transpose8(Y);   // consume ycur before its registers are reloaded
-    if constexpr (!kBjLateRead) {
-      // source i+1: its DMA (issued kBjRing-2 iterations ago) has landed once only the DMAs of
-      // i+2 .. i+kBjRing-2 remain; start its LDS read now, consume it next iteration
-      vm_wait<2 * (kBjRing - 3)>();
-      ring_read(ring_p + ((i + 1) % kBjRing) * kBjSlot, lane, ycur);
-    }
-    {   // refill the slot of source i-1 (read and consumed) with source i + kBjRing - 1
-      if constexpr (!(ABL & 64))
-        dma_source(nrow + x0, nrow + x1, ring + ((i + kBjRing - 1) % kBjRing) * kBjSlot);
-      if constexpr (DEC)
-        nrow = reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i + kBjRing));
-      else
-        nrow += (i + kBjRing < k) ? stride : 0u;
-    }
-    // offsets of source i+1, loaded before the chain so their latency hides behind it (loading
-    // them after the chain into the same registers saves the copies but measured 10 % slower)
-    next_offsets(i);
-    if constexpr (!(ABL & 2)) {
-      NTC_BJ_TABLES(Y)
-    } else if constexpr (GX >= 3) {   // timing ablation: source 0's tables for every source
-      if (i == 0) {
-        NTC_BJ_TABLES(Y)
-#pragma unroll
-        for (int n = 8; n < kBjPlanes; ++n) Yk[n] = Y[n];
-      }
-#pragma unroll
-      for (int n = 8; n < kBjPlanes; ++n) Y[n] = Yk[n];
-    } else {
-#pragma unroll
-      for (int n = 8; n < kBjPlanes; ++n) Y[n] = Y[n & 7] + n;
-    }
-    if constexpr (GX == 1) {
-      const uint64_t P0 = (static_cast<uint64_t>(o[0][1]) << 32) | o[0][0];   // rows 0-3
-      const uint64_t P1 = (static_cast<uint64_t>(o[0][3]) << 32) | o[0][2];   // rows 4-7
-      asm volatile(NTC_GX_CHAIN : NTC_GX_OUTS(A) : NTC_GX_INS(Y, P0, P1) : NTC_GX_CLOBBERS);
-      continue;
-    } else if constexpr (GX == 2) {
-      const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
-      asm volatile(NTC_GX2_CHAIN : NTC_GX_OUTS(A) : NTC_GX2_INS(Y, P) : NTC_GX2_CLOBBERS);
-      continue;
-    } else if constexpr (GX == 3 && kGxLean) {
-      // lean entry: the coefficient pair and the table base arrive in the registers the chain
-      // uses (s[90:91], s[96:97]), and an all-zero pair needs no test (its block 0 has no VALU
-      // and its tail returns at once).  M0 (compiler-reserved) is still saved and restored.
-      uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
-      asm volatile("s_mov_b32 s94, m0\n"
-                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-                   "s_lshl_b32 s98, s90, 24\n"
-                   "s_lshr_b32 s98, s98, 17\n"
-                   "s_add_u32 s98, s96, s98\n"
-                   "s_addc_u32 s99, s97, 0\n"
-                   "s_swappc_b64 s[92:93], s[98:99]\n"
-                   "s_set_gpr_idx_off\n"
-                   "s_mov_b32 m0, s94\n"
-                   : NTC_GX_OUTS(A), [p] "+{s[90:91]}"(P)
-                   : NTC_GX3_YPINS(Y), [tb] "{s[96:97]}"(tbase)
-                   : "s92", "s93", "s94", "s98", "s99", "scc");
-      continue;
-    } else if constexpr (GX == 3) {
-      const uint64_t P = ((static_cast<uint64_t>(o[0][1]) << 32) | o[0][0]) & pmask;
-      asm volatile("s_mov_b32 s94, m0\n"
-                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-                   "s_mov_b64 s[96:97], %[tb]\n"
-                   "s_mov_b64 s[90:91], %[p]\n"
-                   "s_cmp_eq_u64 s[90:91], 0\n"
-                   "s_cbranch_scc1 LT3d%=\n"
-                   "s_lshl_b32 s98, s90, 24\n"
-                   "s_lshr_b32 s98, s98, 17\n"
-                   "s_add_u32 s98, s96, s98\n"
-                   "s_addc_u32 s99, s97, 0\n"
-                   "s_swappc_b64 s[92:93], s[98:99]\n"
-                   "LT3d%=:\n"
-                   "s_set_gpr_idx_off\n"
-                   "s_mov_b32 m0, s94\n"
-                   : NTC_GX_OUTS(A)
-                   : NTC_GX3_YPINS(Y), [p] "s"(P), [tb] "s"(tbase)
-                   : "s90", "s91", "s92", "s93", "s94", "s96", "s97", "s98", "s99", "scc");
-      continue;
-    } else {
-    uint32_t O[16 * NJ];
-#pragma unroll
-    for (int s = 0; s < 16 * NJ; ++s) O[s] = o[s >> 4][s & 15];
-    if constexpr ((ABL & 4) != 0) {   // straight-line stand-in for the chain: 16 VALU per row
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-#pragma unroll
-        for (int p = 0; p < 8; ++p) {
-          acc[j][p] = bxor3(acc[j][p], Y[(j + p) % kBjPlanes], Y[(j + 2 * p + 3) % kBjPlanes]);
-          acc[j][p] = bxor3(acc[j][p], Y[(3 * j + p + 7) % kBjPlanes], O[(j + p) & 15]);
-        }
-      continue;
-    }
-    if constexpr ((ABL & 8) != 0) {   // no chain: keep the planes alive with one row's XORs
-#pragma unroll
-      for (int p = 0; p < 8; ++p) acc[0][p] = bxor3(acc[0][p], Y[p + 8], Y[p + 16]) ^ O[p];
-      continue;
-    }
-    if constexpr (R == 16) {
-      asm volatile(NTC_BJ_CHAIN_R16 : NTC_BJ_OUTS_R16(acc) : NTC_BJ_INS_R16(Y, O) : NTC_BJ_CLOBBERS);
-    } else if constexpr (R == 8) {
-      asm volatile(NTC_BJ_CHAIN_R8 : NTC_BJ_OUTS_R8(acc) : NTC_BJ_INS_R8(Y, O) : NTC_BJ_CLOBBERS);
-    } else {
-      asm volatile(NTC_BJ_CHAIN_R4 : NTC_BJ_OUTS_R4(acc) : NTC_BJ_INS_R4(Y, O) : NTC_BJ_CLOBBERS);
-    }
-    }
-  }
-  // Drain the clamped trailing DMAs before the wave's LDS can be handed to another block.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (GX) {
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-#pragma unroll
-      for (int p = 0; p < 8; ++p) acc[j][p] = A[j][p];
-  }
-
-  const uint32_t row0 = tile * RT;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if (static_cast<uint32_t>(j) >= nrows) continue;
-    transpose8(acc[j]);
-    uint8_t* dst;
-    if constexpr (DEC) {
-      const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
-      dst = a.out + static_cast<size_t>(g) * k * stride + uniform(outs[j]) * stride;
-    } else {
-      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
-    }
-    if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-    if (v1) *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
-  }
-}
-
-// Lean loop of the shared-table MAC for full spans (stride % 2048 == 0, k % 4 == 0; gf_mac_bj
-// GX = 4).  The kernel is bound by instruction supply (rocprofv3: ~47 32-byte instruction fetches
-// per source-tile, of which the chain's 8 blocks take 24), so this form trims the per-source
-// loop instead: the loop is unrolled by the ring depth (slot addresses are immediates / loop-
-// invariant SGPRs, no modulo arithmetic), the DMA uses a scalar row base with one lane offset
-// and the instruction offset for the second KiB (which also offsets the LDS address), and it is
-// issued inside the chain's entry block, sharing that block's M0 save / restore.
-__device__ __forceinline__ void dma_full(const uint8_t* row, uint32_t voff, uint32_t slot)
-{
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\t"
-               "s_mov_b32 m0, %3\n\t"
-               "s_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, %2\n\t"
-               "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
-               "s_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(row), "s"(slot) : "memory", "scc");
-}
-
-template <bool DEC>
-__device__ __forceinline__ void mac_tile_bjf(const MacArgs& a, uint32_t g, uint32_t tile,
-                                             uint32_t nrows, uint32_t cc, uint32_t lane,
-                                             uint32_t ring)
-{
-  static_assert(kBjRing == 4, "the unrolled loop assumes a 4-slot ring");
-  const size_t stride = a.stride;
-  const uint32_t k = a.k;
-  const uint32_t voff = cc * 2048u + lane * 16u;       // both KiB of the span lie inside the row
-  const uint32_t rlane = ring + lane * 16u;            // this lane's LDS bytes in slot 0
+  const uint32_t col = cc * 2048u;
+  // One VGPR serves the LDS reads and the (FULL) DMA offsets: x = ring + 16*lane; the DMA's
+  // scalar row base is pre-biased by col - ring.
+  const uint32_t x = ring + lane * 16u;
+  const bool v0 = FULL || col + lane * 16u < stride;
+  const bool v1 = FULL || col + lane * 16u + 1024u < stride;
+  const uint32_t d0 = v0 ? x : ring, d1 = v1 ? x + 1024u : ring;   // !FULL DMA offsets
   const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
-  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBjRing) : nullptr;
-  const uint32_t jstep = a.rp / 4u;
-  const uint32_t* jp = reinterpret_cast<const uint32_t*>(a.coef + static_cast<size_t>(g) * k * a.rp + tile * 8u);
-  const uint64_t pmask = a.rp >= 8 ? ~0ull : 0xFFFFFFFFull;
-  auto row_at = [&](uint32_t i) -> const uint8_t* {    // prologue only; a scalar (SGPR) address
+  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
+  const uint32_t jstep = a.rp;
+  const uint8_t* jp = a.coef + static_cast<size_t>(g) * k * a.rp + tile * R;
+  const uint64_t bias = static_cast<uint64_t>(col) - ring;
+  auto row_at = [&](uint32_t i) -> const uint8_t* {    // a scalar (SGPR) row base, biased
     uint64_t v;
     if constexpr (DEC) v = const_load<uint64_t>(rowp + i);
     else v = reinterpret_cast<uint64_t>(base0 + (i < k ? i : k - 1) * stride);
+    v += bias;
     const uint32_t lo = uniform(static_cast<uint32_t>(v)), hi = uniform(static_cast<uint32_t>(v >> 32));
     return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
   };
   auto lds_row = [&](uint32_t slot, uint32_t (&y)[8]) {
-    const auto* p = reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(rlane + slot * kBjSlot);
+    const auto* p = reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(x + slot * kBsSlot);
     const u32x4 q0 = p[0], q1 = p[1024 / 16];
     y[0] = q0[0]; y[1] = q0[1]; y[2] = q0[2]; y[3] = q0[3];
     y[4] = q1[0]; y[5] = q1[1]; y[6] = q1[2]; y[7] = q1[3];
   };
+  // prologue DMAs (slots 0 .. kBsRing-2): the same instructions as the loop's refill
+  auto dma = [&](const uint8_t* row, uint32_t slot) {
+    uint32_t keep;
+    if constexpr (FULL)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, %2\n\t"
+                   "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(x), "s"(row), "s"(slot) : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, %3\n\t"
+                   "s_add_u32 m0, %4, 0x400\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %2, %3\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(d0), "v"(d1), "s"(row), "s"(slot) : "memory", "scc");
+  };
 
-  u32x8 A[8];
+  u32x8 A[R];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t tbase;
-  asm volatile("s_getpc_b64 s[96:97]\n"
-               "s_add_u32 s96, s96, ntc_gx3_f@rel32@lo+4\n"
-               "s_addc_u32 s97, s97, ntc_gx3_f@rel32@hi+12\n"
-               "s_add_u32 s98, s96, 32768\n"
-               "s_cbranch_scc0 LT3f%=\n"
-               "s_getpc_b64 s[96:97]\n"
-               "s_add_u32 s96, s96, ntc_gx3_s@rel32@lo+4\n"
-               "s_addc_u32 s97, s97, ntc_gx3_s@rel32@hi+12\n"
-               "LT3f%=:\n"
-               "s_mov_b64 %0, s[96:97]\n"
-               : "=s"(tbase) :: "s96", "s97", "s98", "scc");
-  uint32_t slotm[kBjRing];                             // M0 of each slot (loop-invariant SGPRs)
+  for (int j = 0; j < R; ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t tbase = bs_table_base();
+  uint32_t slotm[kBsRing];                             // M0 of each slot (loop-invariant SGPRs)
 #pragma unroll
-  for (int q = 0; q < kBjRing; ++q) slotm[q] = uniform(ring + q * kBjSlot);
+  for (int q = 0; q < kBsRing; ++q) slotm[q] = uniform(ring + q * kBsSlot);
 
 #pragma unroll
-  for (int q = 0; q < kBjRing - 1; ++q) dma_full(row_at(q), voff, slotm[q]);
-  const uint8_t* nrow = row_at(kBjRing - 1);           // the refill of iteration 0
-  u32x2 on = const_load<u32x2>(jp);
+  for (int q = 0; q < kBsRing - 1; ++q) dma(row_at(q), slotm[q]);
+  const uint8_t* nrow = row_at(kBsRing - 1);           // the refill of iteration 0
+  CoefV on = const_load<CoefV>(jp);
   uint32_t ycur[8];
-  vm_wait<2 * (kBjRing - 2)>();
-  lds_row(0, ycur);
-  for (uint32_t i0 = 0; i0 < k; i0 += kBjRing) {
+  if constexpr (!kLate) {
+    vm_wait<2 * (kBsRing - 2)>();
+    lds_row(0, ycur);
+  }
+  for (uint32_t i0 = 0; i0 < k; i0 += kBsRing) {
 #pragma unroll
-    for (int u = 0; u < kBjRing; ++u) {
+    for (int u = 0; u < kBsRing; ++u) {
       const uint32_t i = i0 + u;
-      const u32x2 o = on;
-      uint32_t Y[kBjPlanes];
+      if (i >= k) break;                               // uniform: k % 4 != 0
+      const CoefV o = on;
+      uint32_t Y[kBsPlanes];
+      if constexpr (kLate) {
+        vm_wait<2 * (kBsRing - 2)>();                  // source i has landed
+        lds_row(u, ycur);
+      }
 #pragma unroll
       for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
       transpose8(Y);
-      vm_wait<2 * (kBjRing - 3)>();                    // source i+1 has landed
-      lds_row((u + 1) % kBjRing, ycur);
+      if constexpr (!kLate) {
+        vm_wait<2 * (kBsRing - 3)>();                  // source i+1 has landed
+        lds_row((u + 1) % kBsRing, ycur);
+      }
       jp += (i + 1 < k) ? jstep : 0u;
-      on = const_load<u32x2>(jp);
-      NTC_BJ_TABLES(Y)
-      uint64_t P = ((static_cast<uint64_t>(o[1]) << 32) | o[0]) & pmask;
+      on = const_load<CoefV>(jp);
+      NTC_BS_TABLES(Y)
+      uint64_t P0 = (static_cast<uint64_t>(o[1]) << 32) | o[0];
+      const uint32_t slot = slotm[(u + kBsRing - 1) % kBsRing];
+      // decode: the next refill's row address, loaded before the chain so its latency hides
+      const uint8_t* nrow_next = DEC ? row_at(i + kBsRing) : nrow + ((i + kBsRing < k) ? stride : 0u);
       // refill the slot of source i-1 with source i+3, then the chain (one M0 save / restore)
-      asm volatile("s_mov_b32 s94, m0\n"
-                   "s_mov_b32 m0, %[slot]\n"
-                   "s_nop 0\n"
-                   "global_load_lds_dwordx4 %[voff], %[row]\n"
-                   "global_load_lds_dwordx4 %[voff], %[row] offset:1024\n"
-                   "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-                   "s_lshl_b32 s98, s90, 24\n"
-                   "s_lshr_b32 s98, s98, 17\n"
-                   "s_add_u32 s98, s96, s98\n"
-                   "s_addc_u32 s99, s97, 0\n"
-                   "s_swappc_b64 s[92:93], s[98:99]\n"
-                   "s_set_gpr_idx_off\n"
-                   "s_mov_b32 m0, s94\n"
-                   : NTC_GX_OUTS(A), [p] "+{s[90:91]}"(P)
-                   : NTC_GX3_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slotm[(u + kBjRing - 1) % kBjRing]),
-                     [voff] "v"(voff), [row] "s"(nrow)
-                   : "s92", "s93", "s94", "s98", "s99", "scc", "memory");
-      if constexpr (DEC) nrow = reinterpret_cast<const uint8_t*>(const_load<uint64_t>(rowp + i + kBjRing));
-      else nrow += (i + kBjRing < k) ? stride : 0u;
+#define NTC_BS_DMA_FULL \
+      "s_mov_b32 s94, m0\n" "s_mov_b32 m0, %[slot]\n" "s_nop 0\n" \
+      "global_load_lds_dwordx4 %[x], %[row]\n" "global_load_lds_dwordx4 %[x], %[row] offset:1024\n"
+#define NTC_BS_DMA_PART \
+      "s_mov_b32 s94, m0\n" "s_mov_b32 m0, %[slot]\n" "s_nop 0\n" \
+      "global_load_lds_dwordx4 %[d0], %[row]\n" "s_add_u32 m0, %[slot], 0x400\n" "s_nop 0\n" \
+      "global_load_lds_dwordx4 %[d1], %[row]\n"
+#define NTC_BS_ENTER \
+      "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n" \
+      "s_lshl_b32 s98, s90, 24\n" "s_lshr_b32 s98, s98, 17\n" \
+      "s_add_u32 s98, s96, s98\n" "s_addc_u32 s99, s97, 0\n" \
+      "s_swappc_b64 s[92:93], s[98:99]\n"
+#define NTC_BS_SECOND \
+      "s_mov_b64 s[90:91], %[p1]\n" "s_cmp_eq_u64 s[90:91], 0\n" "s_cbranch_scc1 LBS2%=\n" \
+      "s_set_gpr_idx_idx 64\n" \
+      "s_lshl_b32 s98, s90, 24\n" "s_lshr_b32 s98, s98, 17\n" \
+      "s_add_u32 s98, s96, s98\n" "s_addc_u32 s99, s97, 0\n" \
+      "s_swappc_b64 s[92:93], s[98:99]\n" "LBS2%=:\n"
+#define NTC_BS_LEAVE "s_set_gpr_idx_off\n" "s_mov_b32 m0, s94\n"
+#define NTC_BS_CLOB "s92", "s93", "s94", "s98", "s99", "scc", "memory"
+      if constexpr (R == 8) {
+        if constexpr (FULL)
+          asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_LEAVE
+                       : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
+                       : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [x] "v"(x),
+                         [row] "s"(nrow)
+                       : NTC_BS_CLOB);
+        else
+          asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_LEAVE
+                       : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
+                       : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
+                         [d1] "v"(d1), [row] "s"(nrow)
+                       : NTC_BS_CLOB);
+      } else {
+        const uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];
+        if constexpr (FULL)
+          asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
+                       : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
+                       : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [x] "v"(x),
+                         [row] "s"(nrow), [p1] "s"(P1)
+                       : NTC_BS_CLOB);
+        else
+          asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
+                       : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
+                       : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
+                         [d1] "v"(d1), [row] "s"(nrow), [p1] "s"(P1)
+                       : NTC_BS_CLOB);
+      }
+      nrow = nrow_next;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped trailing DMAs
 
-  const uint32_t row0 = tile * 8u;
-  const uint32_t c0 = voff, c1 = voff + 1024u;
+  const uint32_t row0 = tile * R;
+  const uint32_t c0 = col + lane * 16u, c1 = c0 + 1024u;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < R; ++j) {
     if (static_cast<uint32_t>(j) >= nrows) continue;
     uint32_t acc[8];
 #pragma unroll
@@ -864,32 +618,24 @@ __device__ __forceinline__ void mac_tile_bjf(const MacArgs& a, uint32_t g, uint3
     } else {
       dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
     }
-    *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-    *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+    if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+    if (v1) *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
   }
 }
 
-// One wave per (generation, RT-row tile, 2 KiB column span).  Blocks are renumbered so that each
+// One wave per (generation, R-row tile, 2 KiB column span).  Blocks are renumbered so that each
 // XCD (block b runs on XCD b % 8) owns a contiguous range of tasks: the row tiles of one
 // generation then share that XCD's L2 instead of each pulling the sources from HBM.
-#ifndef NTC_BJ_WPB
-#define NTC_BJ_WPB 4
-#endif
-constexpr int kBjWaves = NTC_BJ_WPB;     // waves (independent tasks) per workgroup; tuning builds
-
-template <int RT, bool DEC, int ABL = 0, int GX = 0>
-#ifndef NTC_BJ_WAVES_PER_EU
-#define NTC_BJ_WAVES_PER_EU 1
-#endif
-__global__ __launch_bounds__(64 * kBjWaves)
-__attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_mac_bj(MacArgs a)
+template <int R, bool DEC, bool FULL>
+__global__ __launch_bounds__(64 * kBsWaves)
+__attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
 {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kBjWaves * kBjRing * kBjSlot];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kBsWaves * kBsRing * kBsSlot];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t nb = gridDim.x;                       // a multiple of 8 (launch_mac)
   const uint32_t b = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
-  uint32_t task = uniform(b * kBjWaves + wave);
+  uint32_t task = uniform(b * kBsWaves + wave);
   // few generations (dense, G = 1): row tiles fastest, so an XCD owns whole column spans and its
   // L2 serves each source slice to every row tile; many generations: column spans fastest
   uint32_t cc, tile;
@@ -907,51 +653,15 @@ __attribute__((amdgpu_waves_per_eu(RT == 8 ? NTC_BJ_WAVES_PER_EU : 1))) void gf_
   const uint32_t g = task;
   if (g >= a.G) return;
   const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
-  const uint32_t row0 = tile * RT;
+  const uint32_t row0 = tile * R;
   if (row0 >= total) return;
-  const uint32_t nrows = min(static_cast<uint32_t>(RT), total - row0);
-  const uint8_t* ring_p = s_ring + wave * (kBjRing * kBjSlot);
-  const uint32_t ring = lds_addr(ring_p);
-  if constexpr (RT == 16) {
-    if (nrows > 8) {
-      mac_tile_bj<16, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
-      return;
-    }
-  }
-  if constexpr (GX == 4) {
-    mac_tile_bjf<DEC>(a, g, tile, nrows, cc, lane, ring);
-    return;
-  } else if constexpr (GX != 0) {
-    mac_tile_bj<8, RT, DEC, ABL, GX>(a, g, tile, nrows, cc, lane, ring_p, ring);
-    return;
-  }
-  if (nrows > 4) mac_tile_bj<8, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
-  else mac_tile_bj<4, RT, DEC, ABL>(a, g, tile, nrows, cc, lane, ring_p, ring);
-}
-
-// Shared-table chain offsets: per (generation, source, 8-row tile) the 8 rows' kGxOff[c] as u16,
-// from the coefficient bytes coef[g][i][rp] (rows >= rp read as 0).  One thread per 16-byte entry.
-__global__ __launch_bounds__(256) void gx_offsets(const uint8_t* __restrict__ coef, uint32_t rp,
-                                                  uint32_t ntiles, uint64_t total,
-                                                  uint32_t* __restrict__ gxo)
-{
-  const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  if (idx >= total) return;
-  const uint32_t tile = static_cast<uint32_t>(idx % ntiles);
-  const uint64_t gi = idx / ntiles;
-  uint32_t w[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t j0 = tile * 8u + 2u * q;
-    const uint32_t c0 = j0 < rp ? coef[gi * rp + j0] : 0u;
-    const uint32_t c1 = j0 + 1 < rp ? coef[gi * rp + j0 + 1] : 0u;
-    w[q] = static_cast<uint32_t>(kGxOff[c0]) | (static_cast<uint32_t>(kGxOff[c1]) << 16);
-  }
-  reinterpret_cast<uint4*>(gxo)[idx] = make_uint4(w[0], w[1], w[2], w[3]);
+  const uint32_t nrows = min(static_cast<uint32_t>(R), total - row0);
+  const uint32_t ring = lds_addr(s_ring + wave * (kBsRing * kBsSlot));
+  bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring);
 }
 
 // Input row address of every plan position for the bit-sliced decode MAC: position i < k reads
-// received source slot plan_in[i] (< k) or repair plan_in[i] - k; entries k .. k + kBjRing - 1
+// received source slot plan_in[i] (< k) or repair plan_in[i] - k; entries k .. k + kBsRing - 1
 // repeat position k - 1 (the MAC's ring prefetches run past the last source).  Generations with
 // nothing to decode are skipped (the MAC does not read them).
 __global__ __launch_bounds__(256) void plan_rows(const uint16_t* __restrict__ plan_m,
@@ -960,7 +670,7 @@ __global__ __launch_bounds__(256) void plan_rows(const uint16_t* __restrict__ pl
                                                  const uint8_t* src, const uint8_t* rep,
                                                  uint64_t* __restrict__ rows)
 {
-  const uint32_t kp = k + kBjRing;
+  const uint32_t kp = k + kBsRing;
   const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
   if (idx >= static_cast<uint64_t>(G) * kp) return;
   const uint32_t g = static_cast<uint32_t>(idx / kp), i = static_cast<uint32_t>(idx % kp);
@@ -1016,8 +726,6 @@ struct PrepArgs {
   uint8_t* coef;
   uint16_t* rep_size;
   uint16_t* rep_len;
-  uint32_t* joff;      // non-null: write the bit-sliced MAC's jump offsets (8-row tiles) instead
-  uint32_t ntiles;     //   of the coefficient bytes (bj_offsets fused into the preparation)
 };
 
 __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
@@ -1025,35 +733,20 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
   const uint32_t g = blockIdx.x;
   const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
   const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
-  // LDS copies of the v_perm tables (encoded sizes) and of the block offsets (jump offsets).
-  // Small generations (k * r < 1024: under 4 size lookups per thread) read the tables from the
-  // constant bank instead: cheaper than an 8 KiB copy and a barrier per block (k=32 r=8:
-  // 0.0115 -> 0.0100 ms per batch; k=128 r=32 keeps the copy: 0.030 vs 0.043 ms without it)
+  // LDS copy of the v_perm tables (encoded sizes).  Small generations (k * r < 1024: under 4
+  // size lookups per thread) read the tables from the constant bank instead: cheaper than an
+  // 8 KiB copy and a barrier per block (k=32 r=8: 0.0115 -> 0.0100 ms per batch; k=128 r=32
+  // keeps the copy: 0.030 vs 0.043 ms without it)
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
-  __shared__ uint32_t vo[16];
-  const bool lds_tabs = a.joff || a.k * a.r >= 1024u;
+  const bool lds_tabs = a.k * a.r >= 1024u;
   if (lds_tabs) {                                 // uniform
     const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
     for (uint32_t i = threadIdx.x; i < 512u; i += 256u) dst[i] = src[i];
-    if (threadIdx.x < 16) vo[threadIdx.x] = kBjVo[threadIdx.x];
     __syncthreads();
   }
   const uint32_t (*tabs)[8] = lds_tabs ? ptab : d_perm.w;
-  if (a.joff) {
-    // 4 sites (2 rows x 2 nibbles) per thread and step, like bj_offsets
-    uint4* jo = reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * a.k * a.ntiles * 16u);
-    const uint32_t n4 = a.k * a.ntiles * 4u;
-    for (uint32_t t = threadIdx.x; t < n4; t += 256) {
-      const uint32_t qd = t & 3u, tile = (t >> 2) % a.ntiles, i = (t >> 2) / a.ntiles;
-      const uint32_t j0 = tile * 8u + 2u * qd;
-      const uint32_t c0 = j0 < a.r ? coefficient(ridb + j0, sidb + i) : 0u;
-      const uint32_t c1 = j0 + 1 < a.r ? coefficient(ridb + j0 + 1, sidb + i) : 0u;
-      const uint32_t s0 = 4u * qd * kBjSite;
-      jo[t] = make_uint4(s0 + vo[c0 & 15u], s0 + kBjSite + vo[c0 >> 4],
-                         s0 + 2u * kBjSite + vo[c1 & 15u], s0 + 3u * kBjSite + vo[c1 >> 4]);
-    }
-  } else {
+  {
     uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp;
     const uint32_t n = a.k * a.rp;
     for (uint32_t t = threadIdx.x * 4; t < n; t += 256 * 4) {
@@ -1123,9 +816,6 @@ struct PlanArgs {
   uint16_t* plan_out;
   uint8_t* plan_coef;
   uint32_t rp;
-  uint32_t ablate;   // tuning only: bit0 skip elimination, bit1 skip D for received sources
-  uint32_t* joff;    // non-null: also write the bit-sliced MAC's jump offsets (8-row tiles)
-  uint32_t ntiles;
   uint32_t big_rows, big_pitch;   // decode_plan_big: LDS matrix shape
   // decode_plan_w, when non-null: also write the decode MAC's input row addresses (what
   // plan_rows computes at apply time) for the buffers the apply will use
@@ -1137,17 +827,6 @@ struct PlanArgs {
   uint32_t deferred_only;         // decode_plan_big: only the generations an m_cap pass deferred
 };
 
-// Jump offsets of one (input position, 8-row tile, 2-row quad) from the two rows' coefficients
-// (the layout bj_offsets writes).
-__device__ __forceinline__ uint4 bj_quad(uint32_t qd, uint32_t c0, uint32_t c1)
-{
-  const uint32_t s0 = 4u * qd * kBjSite;
-  return make_uint4(s0 + kBjVo[c0 & 15u], s0 + kBjSite + kBjVo[c0 >> 4],
-                    s0 + 2u * kBjSite + kBjVo[c1 & 15u], s0 + 3u * kBjSite + kBjVo[c1 >> 4]);
-}
-
-
-
 // D column of one received-source position j (one lane): D[s][j] = sum_q (M^-1)[s][q] * c(q, j)
 // for the R (padded) output rows s.  The lane's coefficient c(q, j) selects its own v_perm table
 // (one 32-byte row of d_perm per q); the wave-uniform bytes (M^-1)[s..s+3][q] are the data, so one
@@ -1156,7 +835,7 @@ __device__ __forceinline__ uint4 bj_quad(uint32_t qd, uint32_t c0, uint32_t c1)
 template <int R, int RM>
 __device__ __forceinline__ void plan_dcol(uint32_t m, uint32_t j, uint32_t sidb,
                                           const uint32_t* rq1, const uint32_t (*minvT)[RM / 4],
-                                          uint8_t* dst, uint32_t rp, uint4* jo, uint32_t ntiles)
+                                          uint8_t* dst, uint32_t rp)
 {
   const uint32_t S1 = sidb + j + 1u;
   uint32_t acc[R / 4];
@@ -1176,16 +855,6 @@ __device__ __forceinline__ void plan_dcol(uint32_t m, uint32_t j, uint32_t sidb,
   for (int w = 0; w < R / 4; ++w)
     if (4u * w < rp) d[w] = acc[w];
   for (uint32_t t = R; t < rp; t += 4) d[t / 4] = 0;
-  if (jo) {                                            // this position's jump offsets
-#pragma unroll
-    for (int s = 0; s < R; s += 2) {
-      if (static_cast<uint32_t>(s / 8) >= ntiles) break;
-      const uint32_t c0 = (acc[s / 4] >> (8 * (s % 4))) & 0xFFu;
-      const uint32_t c1 = (acc[(s + 1) / 4] >> (8 * ((s + 1) % 4))) & 0xFFu;
-      jo[(s / 8) * 4 + (s % 8) / 2] = bj_quad((s % 8) / 2, c0, c1);
-    }
-    for (uint32_t q = (R / 8) * 4; q < ntiles * 4; ++q) jo[q] = bj_quad(q & 3u, 0u, 0u);
-  }
   (void)m;
 }
 
@@ -1226,8 +895,6 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
   const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  if (a.ablate & 8u) return;
-
   uint32_t m = 0;
   for (uint32_t base = 0; base < k; base += 64) {
     const uint32_t idx = base + lane;
@@ -1253,7 +920,6 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
   }
   __syncthreads();
 
-  if (a.ablate & 4u) return;
   ntc_gf256_decode_status st{};
   st.nb_missing = static_cast<uint16_t>(m);
   st.last_repair = 0xFFFF;
@@ -1308,7 +974,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         for (uint32_t w = lane; w < nw; w += 64) A[p][w] = mul4(ti, A[p][w]);
         __syncthreads();
         // eliminate column p from every other row: lane = row, per-lane table of its factor
-        const uint32_t fa = (lane < m && lane != p && !(a.ablate & 1u)) ? (A[lane][pw] >> ps) & 0xFFu : 0u;
+        const uint32_t fa = (lane < m && lane != p) ? (A[lane][pw] >> ps) & 0xFFu : 0u;
         if (fa != 0) {
           uint32_t tf[5];
 #pragma unroll
@@ -1408,14 +1074,6 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
         if (lane < a.rp)
           pc[static_cast<size_t>(q) * a.rp + lane] = static_cast<uint8_t>(lane < m ? minv(lane, q) : 0u);
       }
-      uint4* jo = a.joff ? reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * k * a.ntiles * 16u)
-                         : nullptr;
-      if (jo)
-        for (uint32_t idx = lane; idx < m * a.ntiles * 4u; idx += 64) {
-          const uint32_t q = idx / (a.ntiles * 4u), rem = idx % (a.ntiles * 4u);
-          const uint32_t s0 = (rem / 4u) * 8u + 2u * (rem & 3u);
-          jo[idx] = bj_quad(rem & 3u, s0 < m ? minv(s0, q) : 0u, s0 + 1 < m ? minv(s0 + 1, q) : 0u);
-        }
       if (lane < m) {
         rq1[lane] = ridb + reps[lane] + 1u;
         szs[lane] = rszL[reps[lane]];           // becomes the reduced encoded size of repair q
@@ -1463,19 +1121,15 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
           }
           szs[lane] ^= e;
         }
-        if (!(a.ablate & 2u)) {
-          for (uint32_t p0 = lane; p0 < cnt; p0 += 64) {
-            uint8_t* dst = pc + static_cast<size_t>(pos_base + p0) * a.rp;
-            uint4* jp = jo ? jo + static_cast<size_t>(pos_base + p0) * a.ntiles * 4u : nullptr;
-            const uint32_t j = rl[p0];
-            const uint32_t nt = a.ntiles;
-            if (R == 8 || RM == 8) plan_dcol<8, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
-            else if constexpr (RM >= 16) {
-              if (R == 16 || RM == 16) plan_dcol<16, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
-              else if constexpr (RM >= 32) {
-                if (R == 32 || RM == 32) plan_dcol<32, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
-                else if constexpr (RM >= 64) plan_dcol<64, RM>(m, j, sidb, rq1, minvT, dst, a.rp, jp, nt);
-              }
+        for (uint32_t p0 = lane; p0 < cnt; p0 += 64) {
+          uint8_t* dst = pc + static_cast<size_t>(pos_base + p0) * a.rp;
+          const uint32_t j = rl[p0];
+          if (R == 8 || RM == 8) plan_dcol<8, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+          else if constexpr (RM >= 16) {
+            if (R == 16 || RM == 16) plan_dcol<16, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+            else if constexpr (RM >= 32) {
+              if (R == 32 || RM == 32) plan_dcol<32, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
+              else if constexpr (RM >= 64) plan_dcol<64, RM>(m, j, sidb, rq1, minvT, dst, a.rp);
             }
           }
         }
@@ -1505,7 +1159,7 @@ __global__ __launch_bounds__(64) void decode_plan(PlanArgs a)
 // Large windows (m up to 255, the w = 8 limit): one 256-thread workgroup per
 // generation, the augmented matrix [M | I] (m x 2m bytes) in LDS with thread = row.  Same
 // greedy retry (decoder.cc:448-468), status, decoded sizes (:484-497) and plan layout as
-// decode_plan; the jump offsets of the bit-sliced MAC come from bj_offsets at apply time.
+// decode_plan (the decode MAC reads the plan through plan_rows' row addresses).
 // Windows this large are rare, so this kernel favours simplicity over speed (block barriers per
 // pivot), but every step stays on the device.
 constexpr uint32_t kBigRows = 255;
@@ -1625,7 +1279,7 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
       __syncthreads();
       bool used = false;
       uint32_t mycol = 0;
-      for (uint32_t p = 0; p < m && !(a.ablate & 32u); ++p) {   // bit 32: timing ablation
+      for (uint32_t p = 0; p < m; ++p) {
         const uint32_t x = (tid < m) ? byte_at(tid, p) : 0u;
         const uint32_t q = vote(tid < m && !used && x != 0, p & 1u);
         if (q == 0xFFFFFFFFu) return false;           // uniform: singular
@@ -1641,19 +1295,17 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
         }
         __syncthreads();
       }
-      if (tid < m && !(a.ablate & 32u)) {             // normalise: own pivot entry -> 1
+      if (tid < m) {                                  // normalise: own pivot entry -> 1
         const uint32_t* ti = d_perm.w[field_inv_dev(byte_at(tid, mycol))];
         const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
         for (uint32_t w = 0; w < nw; ++w) A[(tid) * P + (w)] = mul4(tinv, A[(tid) * P + (w)]);
-      } else if (tid < m) {
-        pivrow[tid] = static_cast<uint16_t>(tid);
       }
       __syncthreads();
       return true;
     };
     uint32_t t = m - 1;
     bool ok = attempt(t);
-    if (!ok && t + 1 < nrecv && !(a.ablate & 16u)) {   // bit 16: timing ablation
+    if (!ok && t + 1 < nrecv) {
       // Screening (same outcome as trying t = m, m+1, ... with a full Gauss-Jordan each, as
       // decoder.cc:448-468 does): {first m-1 repairs} + {t} is invertible iff the first m-1 rows
       // are independent and row t is outside their span.  One forward elimination over all
@@ -1744,11 +1396,11 @@ __global__ __launch_bounds__(256) void decode_plan_big(PlanArgs a)
           sl[i] = slen[rl[i]];
         }
         __syncthreads();
-        if (tid < m && !(a.ablate & 128u))     // bit 128: timing ablation
+        if (tid < m)
           for (uint32_t i = 0; i < cnt; ++i) red ^= mul4(ptab[coefficient(rid_t, sidb + rl[i])], sl[i]);
         // 32 positions at a time: thread s takes the table of (M^-1)[s][q] once per q and
         // multiplies four positions' coefficients c(q, j..j+3) per mul4
-        for (uint32_t i0 = 0; i0 < ((a.ablate & 64u) ? 0u : cnt); i0 += 32) {   // bit 64: ablation
+        for (uint32_t i0 = 0; i0 < cnt; i0 += 32) {
           const uint32_t n32 = min(32u, cnt - i0);
           __syncthreads();                      // the previous block's c4 reads are done
           for (uint32_t e = tid; e < m * 8u; e += 256) {
@@ -1991,7 +1643,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   if (m == 0) {
     st.state = 1;
     st.nb_useless = static_cast<uint16_t>(nrecv);
-  } else if (nrecv < m || m > static_cast<uint32_t>(RM) || (a.ablate & 16u)) {
+  } else if (nrecv < m || m > static_cast<uint32_t>(RM)) {
     st.state = 2;
   } else {
     // lane q < nrecv: R1 of the q-th received repair; lane c < m: S1 of missing source c
@@ -2087,7 +1739,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
       for (int w = 0; w < W; ++w) col[w] = orig[w];
       set_byte_dyn<W>(col, m - 1, ct | byte_dyn<W>(orig, m - 1));
-      if ((a.ablate & 1u) || gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
+      if (gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
       if (t == m - 1 && t + 1 < nrecv) t = screen_candidates() - 1;   // the loop's ++t: next
     }
     if (!ok) {
@@ -2102,36 +1754,22 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       st.nb_useless = static_cast<uint16_t>(nrecv - 1 - t);
       st.last_repair = recv[t];
       mm = m;
-      const uint32_t rp = a.rp, ntiles = a.ntiles;
+      const uint32_t rp = a.rp;
       uint16_t* pin = a.plan_in + static_cast<size_t>(g) * k;
       uint8_t* pc = a.plan_coef + static_cast<size_t>(g) * k * rp;
       uint16_t* pout = a.plan_out + static_cast<size_t>(g) * rp;
       uint16_t* slen = a.src_len + static_cast<size_t>(g) * k;
-      uint4* jo0 = a.joff ? reinterpret_cast<uint4*>(a.joff + static_cast<size_t>(g) * k * ntiles * 16u)
-                          : nullptr;
-      // plan row of input position `pos`: the rp coefficient bytes and the MAC's jump offsets
+      // plan row of input position `pos`: the rp coefficient bytes
       auto emit = [&](uint32_t pos, const uint32_t (&v)[W]) {
         uint32_t* d = reinterpret_cast<uint32_t*>(pc + static_cast<size_t>(pos) * rp);
 #pragma unroll
         for (int w = 0; w < W; ++w)
           if (4u * w < rp) d[w] = v[w];
-        if (jo0) {
-          uint4* jo = jo0 + static_cast<size_t>(pos) * ntiles * 4u;
-#pragma unroll
-          for (int s = 0; s < RM; s += 2) {
-            if (static_cast<uint32_t>(s / 8) >= ntiles) break;
-            // ablation bit 2 (timing only): the offsets of zero coefficients, no table lookups
-            const uint32_t c0 = (a.ablate & 4u) ? 0u : (v[s / 4] >> (8 * (s % 4))) & 0xFFu;
-            const uint32_t c1 = (a.ablate & 4u) ? 0u : (v[(s + 1) / 4] >> (8 * ((s + 1) % 4))) & 0xFFu;
-            jo[(s / 8) * 4 + (s % 8) / 2] = bj_quad((s % 8) / 2, c0, c1);
-          }
-        }
       };
       uint32_t LO[W], HI[W];     // this lane's decoded-size terms, low and high length bytes
 #pragma unroll
       for (int w = 0; w < W; ++w) LO[w] = HI[w] = 0;
       auto size_terms = [&](uint32_t len, const uint32_t (&v)[W]) {
-        if (a.ablate & 8u) return;
         uint32_t tl[5], th[5];
         tab(len & 0xFFu, tl);
         tab(len >> 8, th);
@@ -2146,15 +1784,15 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
                           __builtin_amdgcn_perm(th[4], th[4], s2));
           }
       };
-      // input row address of plan position `pos` (plan_rows' layout: k entries, then kBjRing
+      // input row address of plan position `pos` (plan_rows' layout: k entries, then kBsRing
       // copies of the last one, read by the MAC's prefetch)
-      uint64_t* rows_g = a.rows_out ? a.rows_out + static_cast<size_t>(g) * (k + kBjRing) : nullptr;
+      uint64_t* rows_g = a.rows_out ? a.rows_out + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
       auto put_row = [&](uint32_t pos, const uint8_t* row) {
         if (!rows_g) return;
         const uint64_t v = reinterpret_cast<uint64_t>(row);
         rows_g[pos] = v;
         if (pos == k - 1)
-          for (uint32_t e = 0; e < static_cast<uint32_t>(kBjRing); ++e) rows_g[k + e] = v;
+          for (uint32_t e = 0; e < static_cast<uint32_t>(kBsRing); ++e) rows_g[k + e] = v;
       };
       // R1 of the repair in row q (rows 0 .. m-2: received repairs 0 .. m-2; row m-1: repair t)
       const uint32_t t_rid1 = __builtin_amdgcn_readlane(rid1, t);
@@ -2195,7 +1833,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
           uint32_t acc[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) acc[w] = 0;
-          const uint32_t mq = (a.ablate & 2u) ? 0u : m;
+          const uint32_t mq = m;
           // the coefficient table of q+1 is looked up while q's products are formed (its LDS
           // gather is issued after q's selector loads, so their wait leaves it in flight)
           uint32_t tn[5] = {0, 0, 0, 0, 0};
@@ -2313,15 +1951,9 @@ namespace {
 
 uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
-// Column width per lane: widest that still fills most lanes of the last column chunk.
+// Column width per lane of the v_perm MAC.
 int pick_d(uint32_t stride)
 {
-  // NTC_GF256_FORCE_D=1|2|4 overrides the choice (tuning experiments only).
-  static const int forced = [] {
-    const char* v = std::getenv("NTC_GF256_FORCE_D");
-    return v ? std::atoi(v) : 0;
-  }();
-  if ((forced == 1 || forced == 2 || forced == 4) && stride % (4u * forced) == 0) return forced;
   // 8 B per lane measured fastest on MI355X for 1-4 KiB symbols (more waves per SIMD at the same
   // per-coefficient table cost); 4 B only when the stride forces it.
   return stride % 8 == 0 ? 2 : 1;
@@ -2339,62 +1971,47 @@ mac_fn pick_kernel(bool dec, int D)
 // lane), so short symbols leave lanes idle; measured on MI355X it beats the v_perm
 // kernel (8-byte lanes) once >= ~1/3 of its lanes carry data (k=32 r=8, G=8192: 512 B symbols
 // 606 vs 794 GiB/s, 768 B 888 vs 765, 1 KiB 1139 vs 999 -- bit-sliced vs v_perm).
-// NTC_GF256_MAC=perm|bitslice forces one (A/B experiments).
+// ntc_gf256_set_mac_kind forces one (results are identical).
 bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
 {
   if (stride % 16 != 0) return false;
   if (e->mac_kind != NTC_GF256_MAC_AUTO) return e->mac_kind == NTC_GF256_MAC_BITSLICE;
-  static const int forced = [] {
-    const char* s = std::getenv("NTC_GF256_MAC");
-    if (!s) return 0;
-    if (!std::strcmp(s, "perm")) return 1;
-    if (!std::strcmp(s, "bitslice")) return 2;
-    return 0;
-  }();
-  if (forced) return forced == 2;
   const uint32_t pieces = stride / 16, spans = (stride + 2047) / 2048;   // 16-B pieces per span: 128
   return pieces * 100 >= spans * 128 * 33;
 }
 
-// The bit-sliced MAC's chain (gf_bitslice_gidx.inc / gf_bitslice_chain.inc).  Default 3: one
-// shared 256-block table outside the kernels, one dispatch per (source, row), coefficient bytes
-// read directly.  NTC_GF256_BJ_GX=0|1|2 selects the earlier forms for A/B runs: 0 = per-site
-// nibble tables (two dispatches per row), 1 = in-kernel table with packed u16 offsets
-// (gx_offsets kernel), 2 = in-kernel table, coefficient bytes.
-int gx_chain()
+// Bit-sliced MAC kernel for a tile height and span shape.
+mac_fn pick_bs(bool dec, uint32_t rowtile, bool full)
 {
-  static const int gx = [] {
-    const char* v = std::getenv("NTC_GF256_BJ_GX");
-    if (!v) return 3;
-    const int x = std::atoi(v);
-    return x >= 0 && x <= 3 ? x : 3;
-  }();
-  return gx;
+  if (rowtile == 16)
+    return dec ? (full ? gf_mac_bs<16, true, true> : gf_mac_bs<16, true, false>)
+               : (full ? gf_mac_bs<16, false, true> : gf_mac_bs<16, false, false>);
+  return dec ? (full ? gf_mac_bs<8, true, true> : gf_mac_bs<8, true, false>)
+             : (full ? gf_mac_bs<8, false, true> : gf_mac_bs<8, false, false>);
 }
 
 // Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
-// `offsets_ready`: the bit-sliced jump offsets for 8-row tiles are already in e->joff (encode_prep).
-int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what,
-               bool offsets_ready = false)
+int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what)
 {
   mac_fn fn;
-  uint32_t rowtile = 32, span;
+  uint32_t rowtile, span, wpb;
   uint64_t blk_align = 1;
-  if (use_bitslice(e, a.stride) && gx_chain()) {
-    // shared-table chain, 8-row tiles: block offsets from the coefficient bytes (gx_offsets,
-    // variant 1) or the coefficient bytes themselves (variant 2)
-    rowtile = 8;
+  if (use_bitslice(e, a.stride)) {
+    // 16-row tiles (3 waves per SIMD) once a tile has more than 8 rows to fill, else 8-row
+    // tiles (4 waves per SIMD)
+    rowtile = a.rows > 8 ? 16u : 8u;
     span = 2048;
-    blk_align = 8;
-    const int gv = gx_chain();
-    fn = gv == 3 ? (dec ? gf_mac_bj<8, true, 0, 3> : gf_mac_bj<8, false, 0, 3>)
-       : gv == 2 ? (dec ? gf_mac_bj<8, true, 0, 2> : gf_mac_bj<8, false, 0, 2>)
-                 : (dec ? gf_mac_bj<8, true, 0, 1> : gf_mac_bj<8, false, 0, 1>);
-    a.ntiles = (a.rows + 7) / 8;
+    wpb = kBsWaves;
+    blk_align = 8;                              // the kernel's XCD renumbering
+    fn = pick_bs(dec, rowtile, a.stride % 2048 == 0);
     if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)
-      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
+      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBsRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
       if (rc) return rc;
+      // row_ptr now holds these buffers' addresses, not those a plan recorded
+      e->rows_src = nullptr;
+      e->rows_rep = nullptr;
+      e->rows_stride = 0;
       {
         KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
         hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
@@ -2403,109 +2020,18 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       }
       if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
       a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
-    }
-    if (gv == 1) {
-      const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles;
-      int rc = ensure_buf(&e->joff, &e->joff_cap, n * 16, "hipMalloc gx offsets");
-      if (rc) return rc;
-      a.joff = static_cast<const uint32_t*>(e->joff);
-      {
-        KernelTimer kt(e, NTC_GF256_K_BJ_OFFSETS, st);
-        hipLaunchKernelGGL(gx_offsets, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, st,
-                           a.coef, a.rp, a.ntiles, n, static_cast<uint32_t*>(e->joff));
-      }
-      if ((rc = hip_check(hipGetLastError(), "gx_offsets launch"))) return rc;
-    }
-  } else if (use_bitslice(e, a.stride)) {
-    static const uint32_t rt = [] {
-      const char* v = std::getenv("NTC_GF256_BJ_ROWS");      // 8 | 16 (tuning experiments)
-      return (v && std::atoi(v) == 16) ? 16u : 8u;
-    }();
-    rowtile = rt;
-    span = 2048;
-    blk_align = 8;
-    fn = rt == 16 ? (dec ? gf_mac_bj<16, true> : gf_mac_bj<16, false>)
-                  : (dec ? gf_mac_bj<8, true> : gf_mac_bj<8, false>);
-    a.ntiles = (a.rows + rt - 1) / rt;
-    if (dec) {   // input row addresses of the plan positions (MacArgs::row_ptr)
-      const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBjRing);
-      int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
-      if (rc) return rc;
-      {
-        KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
-        hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
-                           a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
-                           a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
-      }
-      if ((rc = hip_check(hipGetLastError(), "plan_rows launch"))) return rc;
-      a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
-    }
-    const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.ntiles * 2u * rt;
-    if (offsets_ready && rt == 8) {
-      // a.joff was set by the caller (encode_prep / decode_plan wrote it)
-    } else {
-      int rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
-      if (rc) return rc;
-      a.joff = static_cast<const uint32_t*>(e->joff);
-      const uint64_t n4 = n / 4;
-      KernelTimer kt(e, NTC_GF256_K_BJ_OFFSETS, st);
-      hipLaunchKernelGGL(bj_offsets, dim3(static_cast<uint32_t>((n4 + 255) / 256)), dim3(256), 0,
-                         st, a.coef, a.rp, rt, a.ntiles, n4, static_cast<uint32_t*>(e->joff));
-      if ((rc = hip_check(hipGetLastError(), "bj_offsets launch"))) return rc;
     }
   } else {
     const int D = pick_d(a.stride);
+    rowtile = 32;
     span = 256u * D;
+    wpb = kWaves;
     fn = pick_kernel(dec, D);
-  }
-  static const int ablate = [] {
-    const char* v = std::getenv("NTC_GF256_BJ_ABLATE");
-    return v ? std::atoi(v) : 0;
-  }();
-  if (ablate && fn == gf_mac_bj<8, false, 0, 3>) {   // timing ablations of the shared-table MAC
-    switch (ablate) {
-      case 1: fn = gf_mac_bj<8, false, 1, 3>; break;
-      case 2: fn = gf_mac_bj<8, false, 2, 3>; break;
-      case 3: fn = gf_mac_bj<8, false, 3, 3>; break;
-      case 16: fn = gf_mac_bj<8, false, 16, 3>; break;
-      case 64: fn = gf_mac_bj<8, false, 64, 3>; break;
-      case 67: fn = gf_mac_bj<8, false, 67, 3>; break;
-      default: break;
-    }
-  }
-  if (ablate && fn == gf_mac_bj<8, false>) {
-    switch (ablate) {
-      case 1: fn = gf_mac_bj<8, false, 1>; break;
-      case 2: fn = gf_mac_bj<8, false, 2>; break;
-      case 3: fn = gf_mac_bj<8, false, 3>; break;
-      case 4: fn = gf_mac_bj<8, false, 4>; break;
-      case 8: fn = gf_mac_bj<8, false, 8>; break;
-      case 11: fn = gf_mac_bj<8, false, 11>; break;
-      case 16: fn = gf_mac_bj<8, false, 16>; break;
-      case 32: fn = gf_mac_bj<8, false, 32>; break;
-      case 64: fn = gf_mac_bj<8, false, 64>; break;
-
-      default: break;
-    }
   }
   a.nrowchunks = (a.rows + rowtile - 1) / rowtile;
   a.ncolchunks = (a.stride + span - 1) / span;
-  static const int order = [] {     // NTC_BJ_ORDER=tile|cc overrides the default (A/B builds)
-    const char* v = std::getenv("NTC_BJ_ORDER");
-    return !v ? -1 : (std::string(v) == "tile" ? 1 : 0);
-  }();
-  a.tile_fast = order >= 0 ? static_cast<uint32_t>(order) : (a.G < 64 ? 1u : 0u);
-  // full 2 KiB spans and k % 4 == 0: the lean-loop form of the shared-table MAC
-  static const bool lean = [] {      // NTC_BJ_FULL=0 keeps the general loop (A/B builds)
-    const char* v = std::getenv("NTC_BJ_FULL");
-    return !v || std::atoi(v) != 0;
-  }();
-  if (lean && a.stride % 2048 == 0 && a.k % 4 == 0 && a.k >= 4) {
-    if (fn == gf_mac_bj<8, false, 0, 3>) fn = gf_mac_bj<8, false, 0, 4>;
-    if (fn == gf_mac_bj<8, true, 0, 3>) fn = gf_mac_bj<8, true, 0, 4>;
-  }
+  a.tile_fast = a.G < 64 ? 1u : 0u;
   const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
-  const uint64_t wpb = rowtile <= 16 ? kBjWaves : kWaves;     // bit-sliced : v_perm kernel
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
@@ -2521,10 +2047,9 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
 
 namespace ntcgpu {
 
-// Coefficient rows padded to the row tile the MAC kernel reads (4, 8, 16 or a multiple of 32).
+// Coefficient rows padded to the row tile the MAC kernels read (8, 16 or a multiple of 32).
 uint32_t tile_rp(uint32_t r)
 {
-  if (r <= 4) return 4;
   if (r <= 8) return 8;
   if (r <= 16) return 16;
   return round_up(r, 32);
@@ -2585,9 +2110,10 @@ const char* ntc_gf256_last_error(void) { return g_err.c_str(); }
 
 const char* ntc_gf256_build_info(void)
 {
-  return "libntc_gf256 gfx950: bit-sliced XOR MAC (32 B lanes, 8-row tiles, one shared 256-block "
-         "table entered per row with VGPR-relative accumulators) for strides filling >= 1/3 of a "
-         "2 KiB wave span; v_perm_b32 3/3/2 split MAC (R in {4,8,16,32}, D in {1,2,4}) otherwise";
+  return "libntc_gf256 gfx950: bit-sliced XOR MAC (32 B lanes, 8- or 16-row tiles, one shared "
+         "256-block table entered per row with VGPR-relative accumulators) for strides filling >= "
+         "1/3 of a 2 KiB wave span; v_perm_b32 3/3/2 split MAC (R in {4,8,16,32}, D in {1,2}) "
+         "otherwise";
 }
 
 uint32_t ntc_gf256_coefficient(uint32_t repair_id, uint32_t src_id) { return coefficient(repair_id, src_id); }
@@ -2631,8 +2157,6 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_out);
   (void)hipFree(e->plan_coef);
   (void)hipFree(e->enc_coef);
-  (void)hipFree(e->joff);
-  (void)hipFree(e->joff_dec);
   (void)hipFree(e->row_ptr);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   for (auto& pair : e->mac_ev)
@@ -2737,6 +2261,10 @@ int ntc_gf256_reserve(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r)
   const uint32_t rp = tile_rp(r);
   int rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   if (rc) return rc;
+  // the decode MAC's input row addresses (decode_plan_w / plan_rows), so later calls never allocate
+  if ((rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<size_t>(G) * (k + kBsRing) * 8,
+                       "hipMalloc row_ptr")))
+    return rc;
   return ensure_plan(e, G, k, rp);
 }
 
@@ -2752,26 +2280,12 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   (void)hipSetDevice(e->device);
   const uint32_t rp = tile_rp(r);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+  if (rc) return rc;
   PrepArgs p{};
   p.G = G; p.k = k; p.r = r; p.rp = rp; p.src_len = src_len; p.sid_base = sid_base;
   p.rid_base = rid_base; p.rep_size = rep_size; p.rep_len = rep_len;
-  // bit-sliced MAC with 8-row tiles: the preparation writes the jump offsets directly
-  static const bool rows16 = [] {
-    const char* v = std::getenv("NTC_GF256_BJ_ROWS");
-    return v && std::atoi(v) == 16;
-  }();
-  const bool fused = use_bitslice(e, stride) && !rows16 && !gx_chain();
-  if (fused) {
-    p.ntiles = (r + 7u) / 8u;
-    const size_t n = static_cast<size_t>(G) * k * p.ntiles * 16u;
-    rc = ensure_buf(&e->joff, &e->joff_cap, n * 4, "hipMalloc joff");
-    if (rc) return rc;
-    p.joff = static_cast<uint32_t*>(e->joff);
-  } else {
-    rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
-    if (rc) return rc;
-    p.coef = static_cast<uint8_t*>(e->enc_coef);
-  }
+  p.coef = static_cast<uint8_t*>(e->enc_coef);
   {
     KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st);
     hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
@@ -2780,8 +2294,7 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
   a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
-  a.joff = static_cast<const uint32_t*>(e->joff);
-  return launch_mac(e, false, a, st, "encode_mac launch", fused);
+  return launch_mac(e, false, a, st, "encode_mac launch");
 }
 
 // rows_src / rows_rep (decode_batch, which knows the apply's buffers): a register plan also
@@ -2789,7 +2302,7 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
 static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, uint16_t* src_len,
                      const uint8_t* src_mask, const uint16_t* rep_size, const uint8_t* rep_mask,
                      const uint32_t* sid_base, const uint32_t* rid_base,
-                     ntc_gf256_decode_status* status, void* stream, bool offsets,
+                     ntc_gf256_decode_status* status, void* stream,
                      const uint8_t* rows_src = nullptr, const uint8_t* rows_rep = nullptr,
                      uint32_t rows_stride = 0)
 {
@@ -2797,18 +2310,10 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     return fail(NTC_GPU_EINVAL, "NULL argument");
   if (G == 0 || k == 0) return fail(NTC_GPU_EINVAL, "G and k must be > 0");
   if (r > kBigRows) return fail(NTC_GPU_EUNSUPPORTED, "r > 255 not supported by decode (w = 8 limit)");
-  // Plan kernel: the engine's plan kind (ntc_gf256_set_plan_kind); under AUTO the environment
-  // variable NTC_GF256_PLAN=lds|big may force one (A/B experiments, process-wide).
-  static const int env_plan = [] {
-    const char* v = std::getenv("NTC_GF256_PLAN");
-    if (v && !std::strcmp(v, "big")) return static_cast<int>(NTC_GF256_PLAN_BIG);
-    if (v && !std::strcmp(v, "lds")) return static_cast<int>(NTC_GF256_PLAN_LDS);
-    return static_cast<int>(NTC_GF256_PLAN_AUTO);
-  }();
-  const int kind = e && e->plan_kind != NTC_GF256_PLAN_AUTO ? e->plan_kind : env_plan;
-  const bool big = r > static_cast<uint32_t>(kMaxPlanRows) || (kind == NTC_GF256_PLAN_BIG && r > 0);
-  if (big) offsets = false;                 // apply computes the bit-sliced offsets (bj_offsets)
   if (k > 65535) return fail(NTC_GPU_EUNSUPPORTED, "k > 65535");
+  // plan kernel: the engine's plan kind (ntc_gf256_set_plan_kind; results are identical)
+  const int kind = e->plan_kind;
+  const bool big = r > static_cast<uint32_t>(kMaxPlanRows) || (kind == NTC_GF256_PLAN_BIG && r > 0);
   const uint32_t rp = tile_rp(r);
   (void)hipSetDevice(e->device);
   int rc = ensure_plan(e, G, k, rp);
@@ -2818,26 +2323,19 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
   p.rep_mask = rep_mask; p.sid_base = sid_base; p.rid_base = rid_base; p.status = status;
   p.plan_m = e->plan_m; p.plan_in = e->plan_in; p.plan_out = e->plan_out;
   p.plan_coef = e->plan_coef; p.rp = rp;
-  if (offsets && r > 0) {
-    p.ntiles = (r + 7u) / 8u;
-    rc = ensure_buf(&e->joff_dec, &e->joff_dec_cap, static_cast<size_t>(G) * k * p.ntiles * 64u,
-                    "hipMalloc joff_dec");
-    if (rc) return rc;
-    p.joff = static_cast<uint32_t*>(e->joff_dec);
-  }
-  static const uint32_t ablate = [] {
-    const char* v = std::getenv("NTC_GF256_PLAN_ABLATE");
-    return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
-  }();
-  p.ablate = ablate;
   // r <= 32: the register-resident plan (four generations per block); PLAN_LDS selects the LDS
   // Gauss-Jordan kernel instead (r > 32 always uses it)
   const bool lds_plan = kind == NTC_GF256_PLAN_LDS;
-  static const uint32_t ablate_w = [] {   // timing ablations of decode_plan_w (results wrong)
-    const char* v = std::getenv("NTC_GF256_PLANW_ABLATE");
-    return v ? static_cast<uint32_t>(std::atoi(v)) : 0u;
-  }();
-  KernelTimer kt(e, NTC_GF256_K_DECODE_PLAN, static_cast<hipStream_t>(stream));
+  const bool wave_plan = !big && r <= 32 && !lds_plan;
+  if (wave_plan && rows_src && rows_rep && use_bitslice(e, rows_stride)) {
+    rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<uint64_t>(G) * (k + kBsRing) * 8,
+                    "hipMalloc row_ptr");
+    if (rc) return rc;
+    p.rows_out = static_cast<uint64_t*>(e->row_ptr);
+    p.rows_src = rows_src;
+    p.rows_rep = rows_rep;
+    p.rows_stride = rows_stride;
+  }
   if (big) {
     static const int lds_ok = [] {
       return static_cast<int>(hipFuncSetAttribute(reinterpret_cast<const void*>(decode_plan_big),
@@ -2845,6 +2343,9 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
                                                   static_cast<int>(big_lds_bytes(260, 129, 256))));
     }();
     if (lds_ok != 0) return fail(NTC_GPU_EDEVICE, "decode_plan_big: LDS attribute");
+  }
+  KernelTimer kt(e, NTC_GF256_K_DECODE_PLAN, static_cast<hipStream_t>(stream));
+  if (big) {
     // matrix rows of 2 * mmax bytes (odd dword pitch), r rows padded so ptab stays 16-B aligned
     auto launch_big = [&](uint32_t mmax, uint32_t cap, uint32_t deferred) {
       p.big_pitch = ((2 * mmax + 3) / 4) | 1u;
@@ -2861,17 +2362,7 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     } else {
       launch_big(r, 0, 0);
     }
-  } else if (r <= 32 && !lds_plan && !ablate) {
-    p.ablate = ablate_w;
-    if (rows_src && rows_rep && use_bitslice(e, rows_stride) && gx_chain()) {
-      rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<uint64_t>(G) * (k + kBjRing) * 8,
-                      "hipMalloc row_ptr");
-      if (rc) return rc;
-      p.rows_out = static_cast<uint64_t*>(e->row_ptr);
-      p.rows_src = rows_src;
-      p.rows_rep = rows_rep;
-      p.rows_stride = rows_stride;
-    }
+  } else if (wave_plan) {
     auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;
     hipLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,
                        static_cast<hipStream_t>(stream), p);
@@ -2880,21 +2371,10 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
   }
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
-  e->last_plan_offsets = p.joff != nullptr;
   e->rows_src = p.rows_out ? rows_src : nullptr;
   e->rows_rep = p.rows_out ? rows_rep : nullptr;
   e->rows_stride = p.rows_out ? rows_stride : 0;
   return hip_check(hipGetLastError(), "decode_plan launch");
-}
-
-// The bit-sliced path with 8-row tiles (the tile shape encode_prep / decode_plan write offsets for).
-static bool bitslice_rt8(const ntc_gf256_engine* e, uint32_t stride)
-{
-  static const bool rows16 = [] {
-    const char* v = std::getenv("NTC_GF256_BJ_ROWS");
-    return v && std::atoi(v) == 16;
-  }();
-  return use_bitslice(e, stride) && !rows16 && !gx_chain();
 }
 
 int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -2903,7 +2383,7 @@ int ntc_gf256_decode_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t 
                           const uint32_t* rid_base, ntc_gf256_decode_status* status, void* stream)
 {
   return plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
-                   stream, false);
+                   stream);
 }
 
 int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -2920,12 +2400,11 @@ int ntc_gf256_decode_apply(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   a.in0 = src; a.in1 = rep; a.out = src;
   a.rows_per_gen = e->plan_m; a.in_idx = e->plan_in; a.out_idx = e->plan_out;
   a.coef = e->plan_coef; a.rp = e->last_rp;
-  const bool ready = e->last_plan_offsets && bitslice_rt8(e, stride);
-  if (ready) a.joff = static_cast<const uint32_t*>(e->joff_dec);
-  // row addresses already written by the plan for exactly these buffers
+  // row addresses already written by the plan for exactly these buffers (launch_mac forgets them
+  // whenever plan_rows overwrites row_ptr for other buffers)
   if (e->rows_src == src && e->rows_rep == rep && e->rows_stride == stride && src)
     a.row_ptr = static_cast<const uint64_t*>(e->row_ptr);
-  return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch", ready);
+  return launch_mac(e, true, a, static_cast<hipStream_t>(stream), "decode_mac launch");
 }
 
 int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r,
@@ -2936,10 +2415,9 @@ int ntc_gf256_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
 {
   int rc = check_shape(G, k, r, stride);
   if (rc) return rc;
-  // the plan also writes the bit-sliced MAC's jump offsets when the apply will use them, and
-  // (register plan, shared-table MAC) the MAC's input row addresses
+  // the register plan also writes the bit-sliced decode MAC's input row addresses
   rc = plan_impl(e, G, k, r, src_len, src_mask, rep_size, rep_mask, sid_base, rid_base, status,
-                 stream, bitslice_rt8(e, stride), src, rep, stride);
+                 stream, src, rep, stride);
   if (rc) return rc;
   return ntc_gf256_decode_apply(e, G, k, r, stride, src, rep, stream);
 }

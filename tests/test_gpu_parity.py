@@ -294,3 +294,36 @@ def test_mac_timing_api(gpu):
         assert ms.value > 0
     finally:
         _native.check(L.ntc_gf256_set_timing(h, 0), "timing")
+
+
+def test_decode_apply_after_other_buffers(gpu, oracle):
+    """decode_batch(A, B) leaves the decode MAC's input row addresses of A / B in the engine (the
+    register plan writes them); decode_apply on other buffers C / D overwrites them (plan_rows),
+    so a later decode_apply(A, B) must not reuse them (advisor r2: a stale row cache read C / D).
+    The last apply must equal the oracle's decode of A / B."""
+    import torch
+    from netcode_amd import BatchDecoder, _native
+    from netcode_amd.engine import Engine, _stream
+    G, k, r, S, m = 16, 64, 16, 4096, 12
+    src, lens = make_sources(G, k, S, S, seed=41)
+    rep, rsz, _ = gpu_encode(gpu, src, lens, k, r)
+    smask = loss_exact_m(G, k, m, seed=42)
+    rmask = np.ones((G, r), np.uint8)
+    lost = src.copy()
+    lost[smask == 0] = 0
+    llen = lens.copy()
+    llen[smask == 0] = 0
+    oout, oolen, ost = oracle.decode_batch(lost, llen, smask, rep, rsz, rmask)
+    A, B = dev(lost, gpu), dev(rep, gpu)
+    BatchDecoder(k, r, gpu)(A, dev(llen, gpu), dev(smask, gpu), B, dev(rsz, gpu), dev(rmask, gpu))
+    torch.cuda.synchronize(gpu)
+    assert (host(A) == oout).all()
+    rng = np.random.default_rng(43)
+    C = dev(rng.integers(0, 256, lost.shape, dtype=np.uint8), gpu)
+    D = dev(rng.integers(0, 256, rep.shape, dtype=np.uint8), gpu)
+    L, h, st = _native.load(), Engine.get(gpu).handle, _stream(gpu)
+    _native.check(L.ntc_gf256_decode_apply(h, G, k, r, S, C.data_ptr(), D.data_ptr(), st), "apply C/D")
+    A.copy_(dev(lost, gpu))
+    _native.check(L.ntc_gf256_decode_apply(h, G, k, r, S, A.data_ptr(), B.data_ptr(), st), "apply A/B")
+    torch.cuda.synchronize(gpu)
+    assert (host(A) == oout).all()

@@ -1,6 +1,5 @@
 """Time the dense inversion (config-5 shape) alone: ntc_gf256_dense_invert_batch on a random
-n x n matrix, mean over --iters launches (HIP events on the engine's stream).  For panel-kernel
-A/B runs (NTC_DENSE_PANEL / NTC_DENSE_ABLATE are read once per process).
+n x n matrix, mean over --iters launches (HIP events on the engine's stream).
 usage: python tools/dense_invert_time.py [--n 1024] [--G 1] [--iters 20]"""
 import argparse
 import json
@@ -32,8 +31,7 @@ def main():
     t1.record()
     torch.cuda.synchronize()
     print(json.dumps({"n": a.n, "G": a.G, "invert_ms": round(t0.elapsed_time(t1) / a.iters, 4),
-                      "ok": int(ok.sum()), "panel": os.environ.get("NTC_DENSE_PANEL", "ra"),
-                      "ablate": os.environ.get("NTC_DENSE_ABLATE", "0")}))
+                      "ok": int(ok.sum())}))
 
 
 if __name__ == "__main__":

@@ -25,7 +25,22 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from gen_bitslice_gidx import byte_ops3, table_planes, NPLANES  # noqa: E402
+from gen_bitslice_table import table_planes, NPLANES, gmul  # noqa: E402
+
+def byte_ops3(lo, hi, c):
+    """acc ^= c * x on v64..v71 (plane operands as %%[yN] placeholders)."""
+    cols = [gmul(c, 1 << q) for q in range(8)]
+    ops = []
+    for p in range(8):
+        a = sum(((cols[q] >> p) & 1) << q for q in range(4))
+        b = sum(((cols[4 + q] >> p) & 1) << q for q in range(4))
+        acc = f"v{64 + p}"
+        if a and b:
+            ops.append(f"v_bitop3_b32 {acc}, {acc}, %%[y{lo[a]}], %%[y{hi[b]}] bitop3:0x96")
+        elif a or b:
+            ops.append(f"v_xor_b32_e64 {acc}, {acc}, %%[y{lo[a] if a else hi[b]}]")
+    return ops
+
 
 Y0 = 32          # table planes v32..v61
 Y0W = 2          # wide variant: planes of group 0 v2..v31, group 1 v32..v61

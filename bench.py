@@ -9,11 +9,10 @@ Multi-GPU (torchrun): every rank owns G independent generations with its own id 
 scaling, no data-path collective); only a barrier and a max-reduce of the timing use RCCL.
 
 Extras in the JSON line:
-* roofline: every MAC kernel of the TIMED steps is bracketed by a HIP event pair on its launch
-  stream (engine timing log, ntc_gf256_timing_log restricted to the MAC kinds), so the dominant
-  kernel's duration comes from the very launches the step time covers; kernels_ms = every kernel
-  of the last 10 warmup steps, run with all launches bracketed (each logged launch costs two
-  event records, microseconds that would distort sub-millisecond timed steps);
+* roofline / kernels_ms: every kernel of the TIMED steps is bracketed by a HIP event pair on its
+  launch stream (engine timing log, ntc_gf256_timing_log), so the dominant kernel's duration and
+  the per-kernel breakdown come from the very launches the step time covers (the event records
+  cost ~1 % of a config-3 step);
 * roofline.traffic / valu_profile: HBM bytes and SQ instruction counts of the same kernel from
   separate rocprofv3 --pmc passes (they cannot run inside this process), labelled with the file
   and the commit they were measured at;
@@ -626,13 +625,13 @@ def main():
     # repetitions (clock ramp experiment, NTC_BENCH_PROBE_FIRST=<reps>)
     probe_reps = int(os.environ.get("NTC_BENCH_PROBE_FIRST", "0"))
     probe = hbm_copy_probe(dev, reps=probe_reps) if probe_reps else None
-    # kernels bracketed by events inside the timed steps: the MACs (plus, for the dense config,
-    # its two inversion/layout launches: 4 ms steps make the event cost negligible)
-    timed_kinds = ("encode_mac", "decode_mac") + (("dense",) if dense else ())
     for _ in range(a.warmup):
         w.step()
     torch.cuda.synchronize(dev)
-    engine.timing_log(a.steps * 16, kinds=timed_kinds)
+    # every kernel of the timed steps is bracketed by a HIP event pair on its launch stream (the
+    # engine's timing log): the roofline kernel and the per-kernel breakdown come from the very
+    # launches the step time covers (the event records cost ~1 % of a config-3 step)
+    engine.timing_log(a.steps * 16)
 
     def barrier():
         if world > 1:
@@ -653,18 +652,6 @@ def main():
     # outputs of the timed steps, checked after the clock stops (warmup runs straight into the
     # timed loop, with no host-side check idling the GPU between them)
     good, ndec, dec_bytes, dec_macs = w.verify()
-    # breakdown of every kernel: nb more steps right after the timed ones (clocks as warm as in
-    # the timed steps), every launch bracketed by an event pair; the MAC kernels of the line come
-    # from the timed steps themselves
-    nb = min(a.steps, 10)
-    engine.timing_log(nb * 16)
-    tb = time.perf_counter()
-    for _ in range(nb):
-        w.step()
-    torch.cuda.synchronize(dev)
-    ms_logged = (time.perf_counter() - tb) / nb * 1e3
-    after_log = engine.timing_read()
-    engine.timing_log(0)
     if world > 1:
         import torch.distributed as dist
         from netcode_amd.shard import max_over_ranks
@@ -673,8 +660,7 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     payload = G * k * S * world
     value = payload / (elapsed / a.steps) / 2**30
-    kern_timed, launches = kernel_summary(log, a.steps, dense)
-    kern = kernel_summary(after_log, nb, dense)[0]    # every kernel, the logged steps after
+    kern_step, launches = kernel_summary(log, a.steps, dense)
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / its mean launch duration
     # over the timed steps.  Encode MAC: read k*S, write r*S per generation; decode MAC: per
@@ -690,10 +676,6 @@ def main():
     achieved = bytes_dom / (t_dom * 1e-3) / 1e9
     traffic, tsrc = pmc_record("pmc_traffic.json", a.config, dom)
     valu, vsrc = pmc_record("pmc_valu.json", a.config, dom)
-    # per-step kernel times: the MAC kernels from the timed steps themselves, the others (prep,
-    # plan, row pointers, dense inversion) from the logged steps after them
-    kern_step = dict(kern)
-    kern_step.update(kern_timed)
     ksum = sum(kern_step.values())
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
@@ -720,12 +702,8 @@ def main():
                           "coefficient schedule (encoded and planned, no decode MAC)",
             "roofline": roof,
             "kernels_ms": {n: round(v, 4) for n, v in sorted(kern_step.items())},
-            "kernels_ms_note": f"per step: {', '.join(sorted(kern_timed))} from the timed steps "
-                               f"(HIP events on every such launch), the other kernels from "
-                               f"{nb} steps run right after the timed ones with every launch "
-                               f"bracketed",
-            "kernels_ms_after_logged": {n: round(v, 4) for n, v in sorted(kern.items())},
-            "ms_per_step_after_logged": round(ms_logged, 4),
+            "kernels_ms_note": "per step, every kernel of the timed steps (HIP event pair on "
+                               "every launch, on its launch stream)",
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_step),
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}

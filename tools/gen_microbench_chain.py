@@ -203,6 +203,24 @@ def main():
             st.append(f"v_bitop3_b32 v{ACC + 8 * j + p}, v{ACC + 8 * j + p}, v{Y0 + (j + p) % 15}, "
                       f"v{Y0 + 15 + (3 * j + p) % 15} bitop3:0x96")
     o.append('#define MB_STRAIGHT \\\n' + "".join(f'  "{l}\\n" \\\n' for l in st) + '  ""')
+    # operand-slot variants of the indexed straight line (M0 += 8 per row): 20 SRC2+DST,
+    # 21 SRC1+DST, 22 DST only, 23 SRC0 only, 24 VOP2 v_xor SRC0+DST (2 ops per plane)
+    slot = {20: ("SRC2,DST", "v{a}, v{y1}, v{y2}, v{a}"), 21: ("SRC1,DST", "v{a}, v{y1}, v{a}, v{y2}"),
+            22: ("DST", "v{a}, v{y1}, v{y2}, v{b}"), 23: ("SRC0", "v{b}, v{a}, v{y1}, v{y2}")}
+    for v in (20, 21, 22, 23, 24):
+        mode = "SRC0,DST" if v == 24 else slot[v][0]
+        st2 = [f"s_set_gpr_idx_on 0, gpr_idx({mode})"]
+        for j in range(8):
+            for p_ in range(8):
+                y1, y2 = Y0 + (j + p_) % 15, Y0 + 15 + (3 * j + p_) % 15
+                if v == 24:
+                    st2.append(f"v_xor_b32 v{ACC + p_}, v{ACC + p_}, v{y1}")
+                else:
+                    ops = slot[v][1].format(a=ACC + p_, b=16 + p_, y1=y1, y2=y2)
+                    st2.append(f"v_bitop3_b32 {ops} bitop3:0x96")
+            st2.append("s_add_u32 m0, m0, 8")
+        st2.append("s_set_gpr_idx_off")
+        o.append(f'#define MB_STRAIGHT_IDX{v} \\\n' + "".join(f'  "{l}\\n" \\\n' for l in st2) + '  ""')
     # the same ops on row 0's registers, VGPR-indexed; M0 += 8 after each row (variant 9) or not (8)
     for v in (8, 9):
         st2 = ["s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)"]
@@ -370,7 +388,14 @@ __global__ __launch_bounds__(256) void mb(const uint64_t* __restrict__ coef, uin
       if constexpr (F == 35) asm volatile(MB_FILL35_16 ::: MB_CLOB16);
       if constexpr (F == 70) asm volatile(MB_FILL70_16 ::: MB_CLOB16);
     }
-    if constexpr (V == 8 || V == 9) {
+    if constexpr (V >= 20 && V <= 24) {
+#define MB_SIDX(N) asm volatile("s_mov_b32 s94, m0\n" MB_STRAIGHT_IDX##N "s_mov_b32 m0, s94" : MB_OUTS8(A) : MB_YINS(Y), "s"(P0) : "s94", "scc", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23")
+      if constexpr (V == 20) MB_SIDX(20);
+      if constexpr (V == 21) MB_SIDX(21);
+      if constexpr (V == 22) MB_SIDX(22);
+      if constexpr (V == 23) MB_SIDX(23);
+      if constexpr (V == 24) MB_SIDX(24);
+    } else if constexpr (V == 8 || V == 9) {
       if constexpr (V == 8) asm volatile("s_mov_b32 s94, m0\n" MB_STRAIGHT_IDX8 "s_mov_b32 m0, s94" : MB_OUTS8(A) : MB_YINS(Y), "s"(P0) : "s94", "scc");
       else asm volatile("s_mov_b32 s94, m0\n" MB_STRAIGHT_IDX9 "s_mov_b32 m0, s94" : MB_OUTS8(A) : MB_YINS(Y), "s"(P0) : "s94", "scc");
     } else if constexpr (V == 0) {
@@ -422,8 +447,10 @@ int main(int argc, char** argv)
   struct Case { const char* name; int v, r, f; kfn fn; };
   Case cases[] = {
     // wide: 8 rows x 64 B per lane (counted as 16 wave-rows of 32 B); fill per 64 B source = 140
-    {"r16low", 12, 16, 0, K<12, 16, 0>()}, {"r16low+fill70", 12, 16, 70, K<12, 16, 70>()},
-    {"product+fill70", 1, 8, 70, K<1, 8, 70>()}, {"product+fill70", 1, 16, 70, K<1, 16, 70>()},
+    {"straight", 0, 8, 0, K<0, 8, 0>()}, {"idx_src0_dst", 9, 8, 0, K<9, 8, 0>()},
+    {"idx_src2_dst", 20, 8, 0, K<20, 8, 0>()}, {"idx_src1_dst", 21, 8, 0, K<21, 8, 0>()},
+    {"idx_dst_only", 22, 8, 0, K<22, 8, 0>()}, {"idx_src0_only", 23, 8, 0, K<23, 8, 0>()},
+    {"idx_vop2_xor", 24, 8, 0, K<24, 8, 0>()},
   };
   Case old_cases[] = {
     {"straight", 0, 8, 0, K<0, 8, 0>()}, {"straight", 0, 16, 0, K<0, 16, 0>()},

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstddef>
 #include <cstdint>
@@ -60,29 +61,36 @@ int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
 // Coefficient rows padded to the MAC kernels' row tile (ntc_gf256_coef_pitch).
 uint32_t tile_rp(uint32_t r);
 
-// Scope guard around one kernel launch: with the timing log on (and room left) records the
-// entry's start event before the launch and its end event when the scope closes, both on the
-// launch stream, so the pair brackets exactly that kernel in stream order.
+// Scope guard around one kernel launch (or a sequence of launches) for the timing log.
+// Single kernels are launched with hipExtLaunchKernelGGL(..., kt.start(), kt.stop(), 0, ...):
+// the dispatch itself stamps the event pair (ext = true), so timing every kernel adds no packets
+// between them.  A multi-launch region (ext = false) is bracketed by event records on the stream
+// instead: the start before the first launch, the end when the scope closes.
 class KernelTimer {
  public:
-  KernelTimer(ntc_gf256_engine* e, uint32_t kind, hipStream_t st) : e_(e), st_(st)
+  KernelTimer(ntc_gf256_engine* e, uint32_t kind, hipStream_t st, bool ext = false)
+      : e_(e), st_(st), ext_(ext)
   {
     if (e_->tlog_n < e_->tlog_cap && ((e_->tlog_mask >> kind) & 1u)) {
       slot_ = static_cast<int>(e_->tlog_n++);
       e_->tlog_kind[slot_] = kind;
-      (void)hipEventRecord(e_->tlog_ev[2 * slot_], st_);
+      if (!ext_) (void)hipEventRecord(e_->tlog_ev[2 * slot_], st_);
     }
   }
   ~KernelTimer()
   {
-    if (slot_ >= 0) (void)hipEventRecord(e_->tlog_ev[2 * slot_ + 1], st_);
+    if (slot_ >= 0 && !ext_) (void)hipEventRecord(e_->tlog_ev[2 * slot_ + 1], st_);
   }
+  // the events an ext launch hands to the dispatch (nullptr: not logged)
+  hipEvent_t start() const { return slot_ >= 0 && ext_ ? e_->tlog_ev[2 * slot_] : nullptr; }
+  hipEvent_t stop() const { return slot_ >= 0 && ext_ ? e_->tlog_ev[2 * slot_ + 1] : nullptr; }
   KernelTimer(const KernelTimer&) = delete;
   KernelTimer& operator=(const KernelTimer&) = delete;
 
  private:
   ntc_gf256_engine* e_;
   hipStream_t st_;
+  bool ext_;
   int slot_ = -1;
 };
 

@@ -520,9 +520,9 @@ int ntc_gf256_dense_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, ui
   if (rc) return rc;
   // combine wants coef[g][i][j] (input-major): the transpose of mat[g][j][i]
   {
-    KernelTimer kt(e, NTC_GF256_K_DENSE, st);
-    hipLaunchKernelGGL(dn_transpose, dim3((k + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, r, k,
-                       pitch, mat, static_cast<uint8_t*>(e->dn_coef));
+    KernelTimer kt(e, NTC_GF256_K_DENSE, st, true);
+    hipExtLaunchKernelGGL(dn_transpose, dim3((k + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st,
+                          kt.start(), kt.stop(), 0, r, k, pitch, mat, static_cast<uint8_t*>(e->dn_coef));
   }
   if ((rc = hip_check(hipGetLastError(), "dn_transpose launch"))) return rc;
   return ntc_gf256_combine_batch(e, G, k, r, stride, src, static_cast<const uint8_t*>(e->dn_coef), rep, stream);

@@ -474,11 +474,10 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   const uint32_t jstep = a.rp;
   const uint8_t* jp = a.coef + static_cast<size_t>(g) * k * a.rp + tile * R;
   const uint64_t bias = static_cast<uint64_t>(col) - ring;
-  auto row_at = [&](uint32_t i) -> const uint8_t* {    // a scalar (SGPR) row base, biased
+  auto row_at = [&](uint32_t i) -> const uint8_t* {    // a scalar (SGPR) row address
     uint64_t v;
     if constexpr (DEC) v = const_load<uint64_t>(rowp + i);
     else v = reinterpret_cast<uint64_t>(base0 + (i < k ? i : k - 1) * stride);
-    v += bias;
     const uint32_t lo = uniform(static_cast<uint32_t>(v)), hi = uniform(static_cast<uint32_t>(v >> 32));
     return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
   };
@@ -515,7 +514,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   for (int q = 0; q < kBsRing; ++q) slotm[q] = uniform(ring + q * kBsSlot);
 
 #pragma unroll
-  for (int q = 0; q < kBsRing - 1; ++q) dma(row_at(q), slotm[q]);
+  for (int q = 0; q < kBsRing - 1; ++q) dma(row_at(q) + bias, slotm[q]);
   const uint8_t* nrow = row_at(kBsRing - 1);           // the refill of iteration 0
   CoefV on = const_load<CoefV>(jp);
   uint32_t ycur[8];
@@ -546,7 +545,10 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       NTC_BS_TABLES(Y)
       uint64_t P0 = (static_cast<uint64_t>(o[1]) << 32) | o[0];
       const uint32_t slot = slotm[(u + kBsRing - 1) % kBsRing];
-      // decode: the next refill's row address, loaded before the chain so its latency hides
+      // the DMA's biased row base, formed here (the scalar load of the row address was issued an
+      // iteration ago, and this block's LDS wait already covered it); then the next refill's row
+      // address, loaded before the chain so its latency hides behind it
+      const uint8_t* row = nrow + bias;
       const uint8_t* nrow_next = DEC ? row_at(i + kBsRing) : nrow + ((i + kBsRing < k) ? stride : 0u);
       // refill the slot of source i-1 with source i+3, then the chain (one M0 save / restore)
 #define NTC_BS_DMA_FULL \
@@ -574,13 +576,13 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
           asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_LEAVE
                        : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [x] "v"(x),
-                         [row] "s"(nrow)
+                         [row] "s"(row)
                        : NTC_BS_CLOB);
         else
           asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_LEAVE
                        : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
-                         [d1] "v"(d1), [row] "s"(nrow)
+                         [d1] "v"(d1), [row] "s"(row)
                        : NTC_BS_CLOB);
       } else {
         const uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];
@@ -588,13 +590,13 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
           asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
                        : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [x] "v"(x),
-                         [row] "s"(nrow), [p1] "s"(P1)
+                         [row] "s"(row), [p1] "s"(P1)
                        : NTC_BS_CLOB);
         else
           asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
                        : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
-                         [d1] "v"(d1), [row] "s"(nrow), [p1] "s"(P1)
+                         [d1] "v"(d1), [row] "s"(row), [p1] "s"(P1)
                        : NTC_BS_CLOB);
       }
       nrow = nrow_next;
@@ -2013,8 +2015,9 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       e->rows_rep = nullptr;
       e->rows_stride = 0;
       {
-        KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st);
-        hipLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
+        KernelTimer kt(e, NTC_GF256_K_PLAN_ROWS, st, true);
+        hipExtLaunchKernelGGL(plan_rows, dim3(static_cast<uint32_t>((nr + 255) / 256)), dim3(256), 0, st,
+                           kt.start(), kt.stop(), 0,
                            a.rows_per_gen, a.in_idx, a.G, a.k, a.rows, static_cast<uint64_t>(a.stride),
                            a.in0, a.in1, static_cast<uint64_t*>(e->row_ptr));
       }
@@ -2036,8 +2039,9 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
   {
-    KernelTimer kt(e, dec ? NTC_GF256_K_DECODE_MAC : NTC_GF256_K_ENCODE_MAC, st);
-    hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, a);
+    KernelTimer kt(e, dec ? NTC_GF256_K_DECODE_MAC : NTC_GF256_K_ENCODE_MAC, st, true);
+    hipExtLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, kt.start(),
+                          kt.stop(), 0, a);
   }
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][1], st);
   return hip_check(hipGetLastError(), what);
@@ -2287,8 +2291,8 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   p.rid_base = rid_base; p.rep_size = rep_size; p.rep_len = rep_len;
   p.coef = static_cast<uint8_t*>(e->enc_coef);
   {
-    KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st);
-    hipLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, p);
+    KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st, true);
+    hipExtLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, kt.start(), kt.stop(), 0, p);
   }
   if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
   MacArgs a{};
@@ -2344,7 +2348,8 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     }();
     if (lds_ok != 0) return fail(NTC_GPU_EDEVICE, "decode_plan_big: LDS attribute");
   }
-  KernelTimer kt(e, NTC_GF256_K_DECODE_PLAN, static_cast<hipStream_t>(stream));
+  // the plan is one launch (a timed ext launch) except the large-window path's two
+  KernelTimer kt(e, NTC_GF256_K_DECODE_PLAN, static_cast<hipStream_t>(stream), !big);
   if (big) {
     // matrix rows of 2 * mmax bytes (odd dword pitch), r rows padded so ptab stays 16-B aligned
     auto launch_big = [&](uint32_t mmax, uint32_t cap, uint32_t deferred) {
@@ -2364,11 +2369,12 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
     }
   } else if (wave_plan) {
     auto* fw = r <= 8 ? decode_plan_w<8> : r <= 16 ? decode_plan_w<16> : decode_plan_w<32>;
-    hipLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,
-                       static_cast<hipStream_t>(stream), p);
+    hipExtLaunchKernelGGL(fw, dim3((G + kPlanWaves - 1) / kPlanWaves), dim3(64 * kPlanWaves), 0,
+                          static_cast<hipStream_t>(stream), kt.start(), kt.stop(), 0, p);
   } else {
     auto* fn = r <= 8 ? decode_plan<8> : r <= 16 ? decode_plan<16> : r <= 32 ? decode_plan<32> : decode_plan<64>;
-    hipLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), p);
+    hipExtLaunchKernelGGL(fn, dim3(G), dim3(64), 0, static_cast<hipStream_t>(stream), kt.start(),
+                          kt.stop(), 0, p);
   }
   e->last_G = G; e->last_k = k; e->last_r = r; e->last_rp = rp;
   e->rows_src = p.rows_out ? rows_src : nullptr;

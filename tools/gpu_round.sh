@@ -11,7 +11,7 @@ tail -1 gpurun_out/$TAG/bench.log
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/$TAG
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- python3 $OLDPWD/bench.py --steps 10 --no-cpu-baseline --no-host-rate > $OUT/prof_bench.log 2>&1) || { tail -20 $OUT/prof_bench.log; exit 1; }
-python tools/trace_timed.py $OUT/prof/run_kernel_trace.csv --timed 10 --total 40 --bench $OUT/prof_bench.log > $OUT/kernel_trace_timed.json
+python tools/trace_timed.py $OUT/prof/run_kernel_trace.csv --timed 10 --total 50 --skip-last 10 --bench $OUT/prof_bench.log > $OUT/kernel_trace_timed.json
 timeout -k 10 300 python bench.py --per-packet > $OUT/per_packet.log 2>&1 || { tail -20 $OUT/per_packet.log; exit 1; }
 tail -1 $OUT/per_packet.log | cut -c1-200
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }

@@ -16,8 +16,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOW = "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --steps 2 --warmup 1 (tools/gpu_pmc.sh)"
-KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
-           "decode_mac": (r"gf_mac_bj<\d+, true", r"gf_mac<\d, true")}
+KERNELS = {"encode_mac": (r"gf_mac_bs<\d+, false", r"gf_mac<\d, false"),
+           "decode_mac": (r"gf_mac_bs<\d+, true", r"gf_mac<\d, true")}
 
 
 def git_head():

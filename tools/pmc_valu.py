@@ -18,8 +18,8 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"encode_mac": (r"gf_mac_bj<\d+, false", r"gf_mac<\d, false"),
-           "decode_mac": (r"gf_mac_bj<\d+, true", r"gf_mac<\d, true")}
+KERNELS = {"encode_mac": (r"gf_mac_bs<\d+, false", r"gf_mac<\d, false"),
+           "decode_mac": (r"gf_mac_bs<\d+, true", r"gf_mac<\d, true")}
 CONFIGS = {"k128r32s4096": (128, 32, 4096, 4096, 32),   # k, r, S, G, m
            "k32r8s1024": (32, 8, 1024, 4096, 8), "k128r32s1500": (128, 32, 1500, 8192, 32)}
 HOW = "rocprofv3 --pmc, 2 SQ passes of bench.py --steps 2 --warmup 1 (tools/gpu_pmc.sh)"

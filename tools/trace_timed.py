@@ -5,7 +5,8 @@ clocks ramp up); the bench times only the last `--steps` steps.  This takes, per
 launches of the last `timed` of `total` steps and prints their time per step next to the
 all-launch mean (a split batch launches its MAC twice per step).
 
-usage: python tools/trace_timed.py <run_kernel_trace.csv> --timed 10 --total 40 [--bench <bench log>]
+usage: python tools/trace_timed.py <run_kernel_trace.csv> --timed 10 --total 50 --skip-last 10
+       [--bench <bench log>]
 """
 import argparse
 import csv
@@ -22,7 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--timed", type=int, required=True, help="timed steps (the trailing ones)")
-    ap.add_argument("--total", type=int, required=True, help="steps in the run (warmup + timed)")
+    ap.add_argument("--total", type=int, required=True, help="steps in the run (warmup + timed + profiled)")
+    ap.add_argument("--skip-last", type=int, default=0, help="trailing steps after the timed ones "
+                    "(bench.py's profiled steps)")
     ap.add_argument("--bench", help="bench log whose JSON line to compare against")
     a = ap.parse_args()
     per = {}
@@ -34,10 +37,11 @@ def main():
         v.sort()
         ds = [d for _, d in v]
         if len(ds) < a.total or not n.startswith(("gf_", "decode_plan", "encode_prep", "plan_rows",
-                                                     "bj_offsets", "dense", "slot_pack", "wire_")):
+                                                     "dense", "slot_pack", "wire_")):
             continue
         lps = len(ds) // a.total                       # launches per step
-        tail = ds[-a.timed * lps:]
+        end = len(ds) - a.skip_last * lps
+        tail = ds[end - a.timed * lps:end]
         out[n] = {"launches": len(ds), "launches_per_step": lps,
                   "mean_all_launches_ms": round(sum(ds) / len(ds), 4),
                   "timed_ms_per_step": round(sum(tail) / a.timed, 4)}

@@ -647,6 +647,9 @@ def main():
     # repetitions (clock ramp experiment, NTC_BENCH_PROBE_FIRST=<reps>)
     probe_reps = int(os.environ.get("NTC_BENCH_PROBE_FIRST", "0"))
     probe = hbm_copy_probe(dev, reps=probe_reps) if probe_reps else None
+    nprof = min(a.steps, 10)
+    engine.timing_log(nprof * 16)        # the log's events exist before the clock starts ...
+    engine.timing_kinds(())              # ... but nothing is logged until the profiled steps
     for _ in range(a.warmup):
         w.step()
     torch.cuda.synchronize(dev)
@@ -666,16 +669,11 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    # outputs of the timed steps, checked after the clock stops (warmup runs straight into the
-    # timed loop, with no host-side check idling the GPU between them)
-    good, ndec, dec_bytes, dec_macs = w.verify()
-    # profiled steps right after (clocks as warm as in the timed ones): every kernel launch timed
-    # by the event pair its dispatch stamps (engine timing log, hipExtLaunchKernelGGL), so the
-    # per-kernel breakdown and the roofline kernel's duration come from these launches, checked
-    # against these steps' own wall time
-    nprof = min(a.steps, 10)
-    engine.timing_log(nprof * 16)
-    torch.cuda.synchronize(dev)
+    # profiled steps straight after (no host work in between, so the clocks stay where the timed
+    # steps left them): every kernel launch timed by the event pair its dispatch stamps (engine
+    # timing log, hipExtLaunchKernelGGL), so the per-kernel breakdown and the roofline kernel's
+    # duration come from these launches, checked against these steps' own wall time
+    engine.timing_kinds(None)
     tp = time.perf_counter()
     for _ in range(nprof):
         w.step()
@@ -683,6 +681,9 @@ def main():
     ms_prof = (time.perf_counter() - tp) / nprof * 1e3
     log = engine.timing_read()
     engine.timing_log(0)
+    # outputs of the last step (the same computation as every timed step), checked after the
+    # clocks stop
+    good, ndec, dec_bytes, dec_macs = w.verify()
     if world > 1:
         import torch.distributed as dist
         from netcode_amd.shard import max_over_ranks

@@ -103,6 +103,9 @@ class Device {
         else std::memcpy(h_coef_ + i * pitch + 4 * s, &coef[i * rows + s], 4);
       }
     }
+#ifdef NTC_CAPI_HOST_STUB
+    std::memset(h_out_, 0, rows * stride);
+#else
     check(hipMemcpyAsync(d_in_, h_in_, nin * stride, hipMemcpyHostToDevice, stream_), "H2D");
     check(hipMemcpyAsync(d_coef_, h_coef_, nin * pitch, hipMemcpyHostToDevice, stream_), "H2D");
     const int rc = w == 8
@@ -114,6 +117,7 @@ class Device {
     if (rc) throw device_error(ntc_gf256_last_error());
     check(hipMemcpyAsync(h_out_, d_out_, rows * stride, hipMemcpyDeviceToHost, stream_), "D2H");
     check(hipStreamSynchronize(stream_), "sync");
+#endif
     for (size_t s = 0; s < rows; ++s) std::memcpy(out[s], h_out_ + s * stride, out_len);
   }
 
@@ -139,6 +143,9 @@ class Device {
         if (w == 8) h_coef_[(g * k + i) * pitch] = static_cast<uint8_t>(c);
         else std::memcpy(h_coef_ + (g * k + i) * pitch, &c, 4);
       }
+#ifdef NTC_CAPI_HOST_STUB
+    std::memset(h_out_, 0, G * stride);
+#else
     check(hipMemcpyAsync(d_in_, h_in_, G * k * stride, hipMemcpyHostToDevice, stream_), "H2D");
     check(hipMemcpyAsync(d_coef_, h_coef_, G * k * pitch, hipMemcpyHostToDevice, stream_), "H2D");
     const int rc = w == 8
@@ -150,6 +157,7 @@ class Device {
     if (rc) throw device_error(ntc_gf256_last_error());
     check(hipMemcpyAsync(h_out_, d_out_, G * stride, hipMemcpyDeviceToHost, stream_), "D2H");
     check(hipStreamSynchronize(stream_), "sync");
+#endif
     for (size_t g = 0; g < G; ++g) sink(g, h_out_ + g * stride);
   }
 
@@ -158,6 +166,10 @@ class Device {
  private:
   Device()
   {
+#ifdef NTC_CAPI_HOST_STUB
+    eng_ = reinterpret_cast<ntc_gf256_engine*>(this);
+    return;
+#endif
     const char* v = std::getenv("NTC_DEVICE");
     const int dev = v ? std::atoi(v) : 0;
     if (ntc_gf256_engine_create(dev, &eng_) != 0) {
@@ -189,8 +201,13 @@ class Device {
       *d = nullptr;
       *h = nullptr;
       *cap = 0;
+#ifdef NTC_CAPI_HOST_STUB
+      *d = std::malloc(n);
+      *h = std::malloc(n);
+#else
       check(hipMalloc(d, n), "hipMalloc");
       check(hipHostMalloc(h, n, hipHostMallocDefault), "hipHostMalloc");
+#endif
       *cap = n;
     };
     up(reinterpret_cast<void**>(&d_in_), reinterpret_cast<void**>(&h_in_), &cap_in_, in_bytes);

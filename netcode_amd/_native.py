@@ -26,6 +26,7 @@ GPU_H_SYMBOLS = [
     "ntc_gf_combine_batch", "ntc_gf_region_multiply", "ntc_gf_coefficient", "ntc_gf_multiply",
     "ntc_gf_invert", "ntc_gf_multiply_size", "ntc_gf256_set_timing", "ntc_gf256_mac_time",
     "ntc_gf256_set_plan_kind", "ntc_gf256_timing_log", "ntc_gf256_timing_read", "ntc_gf256_timing_kinds",
+    "ntc_gf256_gather_combine",
 ]
 
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EDEVICE", 4: "EUNSUPPORTED"}
@@ -72,6 +73,7 @@ def load(path: str | None = None):
     L.ntc_gf256_coef_pitch.argtypes = [u32]
     L.ntc_gf256_coef_pitch.restype = u32
     L.ntc_gf256_combine_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, V]
+    L.ntc_gf256_gather_combine.argtypes = [V, u32, P, P, u32, V]
     L.ntc_gf256_dense_invert_batch.argtypes = [V, u32, u32, P, P, P, V]
     L.ntc_gf256_dense_encode_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, V]
     L.ntc_gf256_dense_decode_batch.argtypes = [V, u32, u32, u32, P, P, P, P, V]

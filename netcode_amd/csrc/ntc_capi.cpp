@@ -9,10 +9,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <list>
 #include <map>
 #include <memory>
@@ -58,6 +60,66 @@ struct Align16 {
 };
 using bytes = std::vector<uint8_t, Align16<uint8_t>>;
 
+// ------------------------------------------------------------------ resident payloads ----
+// The batching adaptor (class Batch below) keeps every payload it combines on the device: a
+// payload is uploaded once, at the first flush that needs it, into a chunk of the device arena,
+// and the results that later combinations read (decoded sources, reduced repairs) stay there too.
+// A chunk is reused once no live payload points into it.
+struct DevChunk {
+  uint8_t* d = nullptr;
+  size_t cap = 0, used = 0;
+  std::atomic<long> live{0};
+};
+
+struct Node;
+using NodeRef = std::shared_ptr<Node>;
+// c * (the first len bytes of node's payload, zero-extended)
+struct Term {
+  NodeRef node;
+  uint32_t c;
+  uint16_t len;
+};
+using Expr = std::vector<Term>;
+
+// A payload: base (bytes handed in or received) or derived (a linear combination of other
+// payloads, evaluated at a batch flush after everything it reads).  Immutable once created.
+struct Node {
+  bytes host;                  // base: the payload; derived: its value once fetched
+  uint16_t size = 0;
+  uint32_t w = 8;              // field of a derived node's coefficients
+  bool derived = false;
+  bool done = false;           // derived: evaluated (on the device, or on the host for w != 8)
+  bool fetched = false;        // derived: value in `host`
+  Expr expr;                   // derived, until evaluated
+  DevChunk* chunk = nullptr;   // device copy: chunk + byte offset (16-byte aligned, zero-padded)
+  uint32_t off = 0;
+  int level = 0;               // flush bookkeeping: evaluation level, visit stamp
+  uint64_t mark = 0;
+  ~Node()
+  {
+    if (chunk) chunk->live.fetch_sub(1, std::memory_order_relaxed);
+  }
+  bool has_value() const { return !derived || fetched; }
+};
+
+inline NodeRef base_node(const uint8_t* p, size_t n)
+{
+  auto nd = std::make_shared<Node>();
+  nd->host.assign(p, p + n);
+  nd->size = static_cast<uint16_t>(n);
+  return nd;
+}
+
+inline NodeRef derived_node(uint32_t w, uint16_t size, Expr&& e)
+{
+  auto nd = std::make_shared<Node>();
+  nd->derived = true;
+  nd->w = w;
+  nd->size = size;
+  nd->expr = std::move(e);
+  return nd;
+}
+
 // ---------------------------------------------------------------------- device engine ----
 // One engine + stream + staging per process.  Encoders and decoders are not thread-safe (like the
 // reference), but distinct objects may live on distinct threads (tests/end_to_end_mt.cc runs an
@@ -66,9 +128,10 @@ class Device {
  public:
   static Device& get()
   {
-    static Device d;
-    if (!d.eng_) throw device_error(d.err_);
-    return d;
+    // never destroyed: payload nodes may outlive static destruction order at process exit
+    static Device* d = new Device;
+    if (!d->eng_) throw device_error(d->err_);
+    return *d;
   }
 
   // out[0..out_len) = sum_i c_i * in_i[0..len_i)  (inputs zero padded), one launch.
@@ -128,6 +191,12 @@ class Device {
   void combine_generations(uint32_t w, size_t G, size_t k, size_t stride, Fill fill, Sink sink)
   {
     std::lock_guard<std::mutex> lock(mu_);
+    combine_generations_locked(w, G, k, stride, fill, sink);
+  }
+
+  template <typename Fill, typename Sink>
+  void combine_generations_body(uint32_t w, size_t G, size_t k, size_t stride, Fill fill, Sink sink)
+  {
     const uint32_t pitch = w == 8 ? ntc_gf256_coef_pitch(1) : 4u;
     grow(G * k * stride, G * k * pitch, G * stride);
     std::memset(h_coef_, 0, G * k * pitch);
@@ -163,7 +232,250 @@ class Device {
 
   uint64_t launches() const { return launches_; }
 
+  // Batch flush: evaluate every derived node the roots need (each after the nodes it reads),
+  // then bring the roots' values to the host.  GF(2^8): payloads on the device arena, one
+  // gather_combine launch per dependency level; other fields: per level one host-staged combine.
+  void evaluate(const std::vector<Node*>& roots)
+  {
+    std::lock_guard<std::mutex> lock(mu_);
+    const uint64_t ep = ++epoch_;
+    std::vector<Node*> todo;                       // dependencies first
+    std::vector<std::pair<Node*, size_t>> stack;
+    for (Node* r : roots) {
+      if (!r->derived || r->done || r->mark == ep) continue;
+      r->mark = ep;
+      stack.push_back({r, 0});
+      while (!stack.empty()) {
+        Node* n = stack.back().first;
+        size_t& i = stack.back().second;
+        if (i < n->expr.size()) {
+          Node* c = n->expr[i++].node.get();
+          if (c->derived && !c->done && c->mark != ep) {
+            c->mark = ep;
+            stack.push_back({c, 0});
+          }
+          continue;
+        }
+        int lv = 1;
+        for (const Term& t : n->expr)
+          if (t.node->derived && !t.node->done) lv = std::max(lv, t.node->level + 1);
+        n->level = lv;
+        todo.push_back(n);
+        stack.pop_back();
+      }
+    }
+    std::stable_sort(todo.begin(), todo.end(), [](const Node* a, const Node* b) { return a->level < b->level; });
+    std::vector<Node*> t8, tw;
+    for (Node* n : todo) (n->w == 8 ? t8 : tw).push_back(n);
+    if (!tw.empty()) evaluate_host(tw);
+    if (!t8.empty() || !roots.empty()) evaluate_w8(t8, roots, ep);
+  }
+
  private:
+  // w != 8: level by level, inputs from the host (the old per-field path)
+  void evaluate_host(const std::vector<Node*>& todo)
+  {
+    for (size_t a = 0; a < todo.size();) {
+      size_t b = a;
+      while (b < todo.size() && todo[b]->level == todo[a]->level && todo[b]->w == todo[a]->w) ++b;
+      size_t kmax = 1, mx = 16;
+      for (size_t i = a; i < b; ++i) {
+        kmax = std::max(kmax, todo[i]->expr.size());
+        mx = std::max<size_t>(mx, todo[i]->size);
+      }
+      combine_generations_locked(todo[a]->w, b - a, kmax, (mx + 15) / 16 * 16,
+          [&](size_t g, size_t i, const uint8_t** ptr, uint16_t* len, uint32_t* c) {
+            const Node* n = todo[a + g];
+            if (i >= n->expr.size()) return false;
+            *ptr = n->expr[i].node->host.data();
+            *len = n->expr[i].len;
+            *c = n->expr[i].c;
+            return true;
+          },
+          [&](size_t g, const uint8_t* sym) {
+            Node* n = todo[a + g];
+            n->host.assign(sym, sym + n->size);
+            n->fetched = n->done = true;
+            n->expr.clear();
+          });
+      a = b;
+    }
+  }
+
+  static size_t pad16(size_t n) { return (std::max<size_t>(n, 1) + 15) / 16 * 16; }
+
+  // a region of `need` bytes in the device arena (bump allocation in the current chunk; a chunk
+  // no live payload points into is reused, else a new one is added)
+  DevChunk* arena_alloc(size_t need, size_t* off)
+  {
+    if (!cur_ || cur_->cap - cur_->used < need) {
+      cur_ = nullptr;
+      for (DevChunk* c : chunks_)
+        if (c->cap >= need && c->live.load(std::memory_order_relaxed) == 0) { cur_ = c; c->used = 0; break; }
+      if (!cur_) {
+        auto* c = new DevChunk;
+        c->cap = std::max<size_t>(need, size_t(16) << 20);
+#ifdef NTC_CAPI_HOST_STUB
+        c->d = static_cast<uint8_t*>(std::malloc(c->cap));
+#else
+        check(hipMalloc(&c->d, c->cap), "hipMalloc arena");
+#endif
+        chunks_.push_back(c);
+        cur_ = c;
+      }
+    }
+    *off = cur_->used;
+    cur_->used += need;
+    return cur_;
+  }
+
+  void evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep)
+  {
+    // base payloads (and host-evaluated ones) the jobs read that are not on the device yet
+    std::vector<Node*> up;
+    size_t up_bytes = 0, out_bytes = 0, nterms = 0;
+    for (Node* n : todo) {
+      nterms += n->expr.size();
+      out_bytes += pad16(n->size);
+      for (const Term& t : n->expr) {
+        Node* c = t.node.get();
+        if (c->chunk || (c->derived && !c->done) || c->mark == ep + (1ull << 63)) continue;
+        c->mark = ep + (1ull << 63);
+        up.push_back(c);
+        up_bytes += pad16(c->size);
+      }
+    }
+    // roots evaluated by an earlier flush (only on the device): fetched one by one below
+    std::vector<Node*> late;
+    size_t late_bytes = 0;
+    for (Node* r : roots)
+      if (r->derived && r->done && !r->fetched && r->chunk) {
+        late.push_back(r);
+        late_bytes += pad16(r->size);
+      }
+    if (todo.empty() && late.empty()) return;
+    size_t base = 0;
+    DevChunk* ch = (up_bytes + out_bytes) ? arena_alloc(up_bytes + out_bytes, &base) : nullptr;
+    grow_stage(up_bytes, out_bytes + late_bytes,
+               todo.size() * sizeof(ntc_gf256_gather_job) + nterms * sizeof(ntc_gf256_gather_term));
+    size_t pos = 0;
+    for (Node* c : up) {
+      std::memcpy(h_up_ + pos, c->host.data(), c->size);
+      std::memset(h_up_ + pos + c->size, 0, pad16(c->size) - c->size);
+      c->chunk = ch;
+      c->off = static_cast<uint32_t>(base + pos);
+      ch->live.fetch_add(1, std::memory_order_relaxed);
+      pos += pad16(c->size);
+    }
+    // jobs (by level) and their terms
+    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_desc_);
+    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_desc_ + todo.size() * sizeof(ntc_gf256_gather_job));
+    size_t ti = 0, opos = base + up_bytes;
+    for (size_t j = 0; j < todo.size(); ++j) {
+      Node* n = todo[j];
+      n->chunk = ch;
+      n->off = static_cast<uint32_t>(opos);
+      ch->live.fetch_add(1, std::memory_order_relaxed);
+      opos += pad16(n->size);
+      jobs[j].out = reinterpret_cast<uint64_t>(ch->d + n->off);
+      jobs[j].term0 = static_cast<uint32_t>(ti);
+      jobs[j].nterms = static_cast<uint32_t>(n->expr.size());
+      jobs[j].len = n->size;
+      jobs[j].pad = 0;
+      for (const Term& t : n->expr) {
+        terms[ti].src = reinterpret_cast<uint64_t>(t.node->chunk->d + t.node->off);
+        terms[ti].len = std::min<uint32_t>(t.len, n->size);
+        terms[ti].coef = t.c;
+        ++ti;
+      }
+    }
+#ifndef NTC_CAPI_HOST_STUB
+    if (up_bytes) check(hipMemcpyAsync(ch->d + base, h_up_, up_bytes, hipMemcpyHostToDevice, stream_), "H2D payloads");
+    const size_t desc = todo.size() * sizeof(ntc_gf256_gather_job) + ti * sizeof(ntc_gf256_gather_term);
+    if (desc) check(hipMemcpyAsync(d_desc_, h_desc_, desc, hipMemcpyHostToDevice, stream_), "H2D jobs");
+    const auto* djobs = reinterpret_cast<const ntc_gf256_gather_job*>(d_desc_);
+    const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(d_desc_ + todo.size() * sizeof(ntc_gf256_gather_job));
+    for (size_t a = 0; a < todo.size();) {
+      size_t b = a;
+      uint32_t mx = 1;
+      while (b < todo.size() && todo[b]->level == todo[a]->level) mx = std::max<uint32_t>(mx, todo[b++]->size);
+      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(b - a), djobs + a, dterms, mx, stream_))
+        throw device_error(ntc_gf256_last_error());
+      a = b;
+    }
+    if (out_bytes)
+      check(hipMemcpyAsync(h_down_, ch->d + base + up_bytes, out_bytes, hipMemcpyDeviceToHost, stream_), "D2H results");
+    std::vector<std::pair<Node*, size_t>> late_pos;
+    size_t lp = out_bytes;
+    for (Node* r : late) {
+      check(hipMemcpyAsync(h_down_ + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
+      late_pos.push_back({r, lp});
+      lp += pad16(r->size);
+    }
+    check(hipStreamSynchronize(stream_), "sync");
+#else
+    std::memset(h_down_, 0, out_bytes);
+    std::vector<std::pair<Node*, size_t>> late_pos;
+#endif
+    ++launches_;
+    for (Node* n : todo) {
+      n->done = true;
+      n->expr.clear();
+    }
+    // the roots' values (results of this flush from the region copy, earlier ones from theirs)
+    for (Node* r : roots) {
+      if (!r->derived || r->fetched) continue;
+      size_t at = 0;
+      bool have = false;
+      if (r->chunk == ch && r->off >= base + up_bytes && r->off < base + up_bytes + out_bytes) {
+        at = r->off - base - up_bytes;
+        have = true;
+      } else {
+        for (const auto& lpp : late_pos)
+          if (lpp.first == r) { at = lpp.second; have = true; }
+      }
+      if (!have) continue;
+      r->host.assign(h_down_ + at, h_down_ + at + r->size);
+      r->fetched = true;
+    }
+  }
+
+  void grow_stage(size_t up, size_t down, size_t desc)
+  {
+    auto up_h = [](uint8_t** h, size_t* cap, size_t need) {
+      if (need <= *cap) return;
+      const size_t n = std::max(need, *cap * 2);
+#ifdef NTC_CAPI_HOST_STUB
+      std::free(*h);
+      *h = static_cast<uint8_t*>(std::malloc(n));
+#else
+      if (*h) (void)hipHostFree(*h);
+      *h = nullptr;
+      check(hipHostMalloc(reinterpret_cast<void**>(h), n, hipHostMallocDefault), "hipHostMalloc");
+#endif
+      *cap = n;
+    };
+    up_h(&h_up_, &cap_up_, up + 16);
+    up_h(&h_down_, &cap_down_, down + 16);
+    up_h(&h_desc_, &cap_desc_, desc + 64);
+    if (desc + 64 > cap_ddesc_) {
+      const size_t n = std::max(desc + 64, cap_ddesc_ * 2);
+#ifdef NTC_CAPI_HOST_STUB
+      std::free(d_desc_);
+      d_desc_ = static_cast<uint8_t*>(std::malloc(n));
+#else
+      if (d_desc_) (void)hipFree(d_desc_);
+      d_desc_ = nullptr;
+      check(hipMalloc(reinterpret_cast<void**>(&d_desc_), n), "hipMalloc jobs");
+#endif
+      cap_ddesc_ = n;
+    }
+  }
+
+  // combine_generations without taking mu_ (the caller holds it)
+  template <typename Fill, typename Sink>
+  void combine_generations_locked(uint32_t w, size_t G, size_t k, size_t stride, Fill fill, Sink sink);
+
   Device()
   {
 #ifdef NTC_CAPI_HOST_STUB
@@ -224,7 +536,19 @@ class Device {
   uint8_t *d_out_ = nullptr, *h_out_ = nullptr;
   size_t cap_in_ = 0, cap_coef_ = 0, cap_out_ = 0;
   uint64_t launches_ = 0;
+  // resident payload arena and its staging (GF(2^8) batches)
+  std::vector<DevChunk*> chunks_;
+  DevChunk* cur_ = nullptr;
+  uint64_t epoch_ = 0;
+  uint8_t *h_up_ = nullptr, *h_down_ = nullptr, *h_desc_ = nullptr, *d_desc_ = nullptr;
+  size_t cap_up_ = 0, cap_down_ = 0, cap_desc_ = 0, cap_ddesc_ = 0;
 };
+
+template <typename Fill, typename Sink>
+void Device::combine_generations_locked(uint32_t w, size_t G, size_t k, size_t stride, Fill fill, Sink sink)
+{
+  combine_generations_body(w, G, k, stride, fill, sink);
+}
 
 // galois_field (galois_field.hh:18-167) for the field size an encoder / decoder was built with:
 // GF(2^8) through the engine's tables, w in {4, 16, 32} through ntc_gf_* (gpu.h).
@@ -339,44 +663,19 @@ namespace ntcx {
 
 // ============================================================================== encoder ====
 class Batch;
-using sym_ptr = std::shared_ptr<const bytes>;
 class Decoder;
-
-// Deferred (batched) symbols are linear expressions over received / produced payloads:
-// sum of c * (the first `len` bytes of *base, zero-extended).  Addition in GF(2^w) is XOR, so
-// terms over the same (base, len) merge by XOR-ing their coefficients.
-struct Term {
-  sym_ptr base;
-  uint32_t c;
-  uint16_t len;
-};
-using Expr = std::vector<Term>;
-
-void expr_add(Expr& dst, const Term& t)
-{
-  if (t.c == 0 || t.len == 0) return;
-  for (auto it = dst.begin(); it != dst.end(); ++it)
-    if (it->base == t.base && it->len == t.len) {
-      it->c ^= t.c;
-      if (it->c == 0) dst.erase(it);
-      return;
-    }
-  dst.push_back(t);
-}
 
 // One event queued in a Batch, emitted at flush in production order: a packet (encoder source,
 // encoder repair whose two symbol copies are filled at flush, decoder ack) or a decoder data
-// delivery (its bytes = expr evaluated at flush, truncated to `size`).
+// delivery (the bytes of `node`, truncated to `size`).
 struct Pending {
   enum Kind { ENC_PACKET, DEC_PACKET, DEC_DATA };
   Kind kind = ENC_PACKET;
   class Encoder* enc = nullptr;
   class Decoder* dec = nullptr;
-  bytes pkt;                           // wire bytes, or the delivered data
-  bool eval = false;                   // expr still to be evaluated
-  uint32_t w = 8;
-  Expr expr;
-  uint16_t size = 0;                   // evaluated length (repair symbol size / data size)
+  bytes pkt;                           // wire bytes
+  NodeRef node;                        // encoder repair / delivered data: the payload to emit
+  uint16_t size = 0;                   // repair symbol size / data size
   size_t off1 = 0, off2 = 0;           // encoder repair: the two symbol copies inside pkt
 };
 
@@ -390,18 +689,21 @@ class Encoder {
   void add_data(bytes&& d)
   {
     if (window_.size() == window_size_) window_.pop_front();
-    window_.push_back(Src{cur_sid_, std::make_shared<const bytes>(std::move(d))});
+    auto nd = std::make_shared<Node>();
+    nd->size = static_cast<uint16_t>(d.size());
+    nd->host = std::move(d);
+    window_.push_back(Src{cur_sid_, std::move(nd)});
     const Src& s = window_.back();
     if (systematic_) {
       ++nb_sources_;
       ++nb_sent_packets_;
       Pending p;
       p.enc = this;
-      begin(p);
+      begin(p, 7 + s.sym->size);
       out_.u8(2);                                  // packetizer.hh:165-183
       out_.u32(s.id);
-      out_.u16(static_cast<uint16_t>(s.sym->size()));
-      out_.raw(s.sym->data(), s.sym->size());
+      out_.u16(s.sym->size);
+      out_.raw(s.sym->host.data(), s.sym->size);
       out_.end();
       finish(std::move(p));
     } else {
@@ -416,47 +718,52 @@ class Encoder {
   void generate_repair()
   {
     if (window_.empty()) throw std::runtime_error("generate_repair on an empty window");
-    std::vector<const uint8_t*> in;
-    std::vector<uint16_t> lens;
-    std::vector<uint32_t> cs;
-    std::vector<uint32_t> ids;
-    Expr terms;
+    ids_.clear();
     uint16_t symsz = 0, esz = 0;
+    Expr terms;
+    if (batch_) terms.reserve(window_.size());
+    else { in_.clear(); lens_.clear(); cs_.clear(); }
     for (const Src& s : window_) {
       const uint32_t c = f_.coef(cur_rid_, s.id);
-      in.push_back(s.sym->data());
-      lens.push_back(static_cast<uint16_t>(s.sym->size()));
-      cs.push_back(c);
-      ids.push_back(s.id);
-      if (batch_) expr_add(terms, Term{s.sym, c, static_cast<uint16_t>(s.sym->size())});
-      symsz = std::max<uint16_t>(symsz, static_cast<uint16_t>(s.sym->size()));
-      esz = static_cast<uint16_t>(f_.msize(static_cast<uint16_t>(s.sym->size()), c) ^ esz);
+      const uint16_t sz = s.sym->size;
+      if (batch_) {
+        terms.push_back(Term{s.sym, c, sz});       // distinct window sources: no merging
+      } else {
+        in_.push_back(s.sym->host.data());
+        lens_.push_back(sz);
+        cs_.push_back(c);
+      }
+      ids_.push_back(s.id);
+      symsz = std::max<uint16_t>(symsz, sz);
+      esz = static_cast<uint16_t>(f_.msize(sz, c) ^ esz);
     }
-    bytes sym(symsz);
-    if (!batch_)
-      Device::get().combine(f_.w, in.size(), in.data(), lens.data(), cs.data(), symsz, sym.data());
+    bytes sym;
+    if (!batch_) {
+      sym.resize(symsz);
+      Device::get().combine(f_.w, in_.size(), in_.data(), lens_.data(), cs_.data(), symsz, sym.data());
+    }
     const uint32_t rid = cur_rid_++;
     ++nb_repairs_;
     ++nb_sent_packets_;
     Pending p;
     p.enc = this;
-    begin(p);
+    begin(p, 15 + 2 * size_t(symsz) + 4 + 3 * ids_.size());
     out_.u8(1);                                    // packetizer.hh:90-122
     out_.u32(rid);
     out_.u16(symsz);
-    p.off1 = p.pkt.size();
-    out_.raw(sym.data(), symsz);
-    out_.ids(ids);
+    p.off1 = batch_ ? p.pkt.size() : 0;
+    if (batch_) p.pkt.resize(p.pkt.size() + symsz);          // filled at flush
+    else out_.raw(sym.data(), symsz);
+    out_.ids(ids_);
     out_.u16(esz);
     out_.u16(symsz);
-    p.off2 = p.pkt.size();
-    out_.raw(sym.data(), symsz);
+    p.off2 = batch_ ? p.pkt.size() : 0;
+    if (batch_) p.pkt.resize(p.pkt.size() + symsz);
+    else out_.raw(sym.data(), symsz);
     out_.end();
     if (batch_) {
-      p.eval = true;
-      p.w = f_.w;
-      p.expr = std::move(terms);
       p.size = symsz;
+      p.node = derived_node(f_.w, symsz, std::move(terms));
     }
     finish(std::move(p));
   }
@@ -513,16 +820,23 @@ class Encoder {
  private:
   struct Src {
     uint32_t id;
-    sym_ptr sym;                       // immutable once in the window (shared with pending repairs)
+    NodeRef sym;                       // immutable once in the window (shared with pending repairs)
   };
   // batch mode: the packet is built into p.pkt (begin) and queued in the batch (finish)
-  void begin(Pending& p) { out_.buf = batch_ ? &p.pkt : nullptr; }
+  void begin(Pending& p, size_t reserve)
+  {
+    out_.buf = batch_ ? &p.pkt : nullptr;
+    if (batch_) p.pkt.reserve(reserve);
+  }
   void finish(Pending&& p);
 
   Field f_;
   Writer out_;
   Batch* batch_ = nullptr;
-  std::list<Src> window_;
+  std::deque<Src> window_;
+  std::vector<uint32_t> ids_, cs_;     // scratch of generate_repair
+  std::vector<const uint8_t*> in_;
+  std::vector<uint16_t> lens_;
   size_t rate_ = 5;
   size_t window_size_ = static_cast<size_t>(-1);
   bool systematic_ = true;
@@ -621,67 +935,44 @@ class Decoder {
  private:
   struct Src {
     uint32_t id;
-    bytes sym;
+    bytes sym;                   // immediate mode
     uint16_t size;
-    Expr expr;                   // batch mode: the symbol as an expression (sym unused)
+    NodeRef node;                // batch mode: the payload (received: base; decoded: derived)
   };
   struct Rep {
     uint32_t id;
     std::vector<uint32_t> ids;   // sorted
     uint16_t esz;
-    bytes sym;
+    bytes sym;                   // immediate mode
     uint16_t symsz;
-    Expr expr;
+    Expr red;                    // batch mode: the reduced repair, its own payload first
   };
 
   void queue(Pending&& p);
-  // evaluate expressions into byte symbols (leaving batch mode): one combine for all of them
-  void materialise(const std::vector<std::pair<Expr*, bytes*>>& todo, const std::vector<uint16_t>& lens)
+  // batch mode: the reduced repair as one payload (its own payload when nothing was removed)
+  NodeRef repair_node(const Rep& r) const
   {
-    size_t kmax = 1, mx = 16;
-    for (size_t g = 0; g < todo.size(); ++g) {
-      kmax = std::max(kmax, todo[g].first->size());
-      mx = std::max<size_t>(mx, lens[g]);
-      for (const Term& t : *todo[g].first) mx = std::max<size_t>(mx, t.len);
-    }
-    if (!todo.empty())
-      Device::get().combine_generations(f_.w, todo.size(), kmax, (mx + 15) / 16 * 16,
-          [&](size_t g, size_t i, const uint8_t** ptr, uint16_t* len, uint32_t* c) {
-            const Expr& e = *todo[g].first;
-            if (i >= e.size()) return false;
-            *ptr = e[i].base->data();
-            *len = e[i].len;
-            *c = e[i].c;
-            return true;
-          },
-          [&](size_t g, const uint8_t* sym) {
-            todo[g].second->assign(sym, sym + std::max<uint16_t>(lens[g], 1));
-            if (lens[g] == 0) (*todo[g].second)[0] = 0;
-            todo[g].first->clear();
-          });
+    if (r.red.size() == 1 && r.red[0].c == 1 && r.red[0].len >= r.symsz) return r.red[0].node;
+    return derived_node(f_.w, r.symsz, Expr(r.red));
   }
-  // batch mode: c * (src truncated to len), added into dst
-  void add_scaled(Expr& dst, const Expr& src, uint32_t c, uint16_t len) const
+  // batch mode: c * (the reduced repair truncated to len), zero-extended to size bytes
+  NodeRef scaled_repair(const Rep& r, uint32_t c, uint16_t len, uint16_t size) const
   {
-    for (const Term& t : src) expr_add(dst, Term{t.base, f_.mul(t.c, c), std::min(t.len, len)});
+    Expr e;
+    e.reserve(r.red.size());
+    for (const Term& t : r.red) e.push_back(Term{t.node, f_.mul(t.c, c), std::min(t.len, len)});
+    return derived_node(f_.w, size, std::move(e));
   }
 
   // decoder.hh:231-248, 292-300
   void deliver(const Src& s)
   {
     if (batch_) {
-      Pending p;
+      Pending p;                 // a received source's own payload, or a decoded one's value
       p.kind = Pending::DEC_DATA;
       p.dec = this;
-      p.w = f_.w;
       p.size = s.size;
-      if (s.expr.size() == 1 && s.expr[0].c == 1 && s.expr[0].len >= s.size) {
-        // a received source: its own payload, no region work
-        p.pkt.assign(s.expr[0].base->begin(), s.expr[0].base->begin() + s.size);
-      } else {
-        p.eval = true;
-        add_scaled(p.expr, s.expr, 1, s.size);
-      }
+      p.node = s.node;
       queue(std::move(p));
     } else {
       dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.sym.data()), s.size);
@@ -729,11 +1020,11 @@ class Decoder {
   void remove_sources_data(Rep& r, const std::vector<const Src*>& known)
   {
     if (known.empty()) return;
-    if (batch_) {
+    if (batch_) {                // one term per source payload, whatever produced it
       for (const Src* s : known) {
         const uint32_t c = f_.coef(r.id, s->id);
         r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
-        add_scaled(r.expr, s->expr, c, std::min<uint16_t>(s->size, r.symsz));
+        r.red.push_back(Term{s->node, c, std::min<uint16_t>(s->size, r.symsz)});
       }
       return;
     }
@@ -757,8 +1048,8 @@ class Decoder {
     const uint32_t inv = f_.inv(f_.coef(r.id, sid));
     const uint16_t sz = f_.msize(r.esz, inv);
     if (batch_) {
-      Src s{sid, bytes(), sz, {}};
-      add_scaled(s.expr, r.expr, inv, std::min(sz, r.symsz));
+      Src s{sid, bytes(), sz, nullptr};
+      s.node = scaled_repair(r, inv, std::min(sz, r.symsz), sz);
       nb_decoded_ += 1;
       return s;
     }
@@ -775,8 +1066,8 @@ class Decoder {
   {
     if (has_last_ && id < last_id_) return;
     if (sources_.count(id)) return;
-    Src s{id, bytes(), sz, {}};
-    if (batch_) s.expr.push_back(Term{std::make_shared<const bytes>(sym, sym + sz), 1, sz});
+    Src s{id, bytes(), sz, nullptr};
+    if (batch_) s.node = base_node(sym, sz);
     else s.sym.assign(sym, sym + sz);
     if (s.sym.empty()) s.sym.resize(1);
     add_source_recursive(std::move(s));
@@ -793,7 +1084,7 @@ class Decoder {
     for (uint32_t sid : ids) if (!sources_.count(sid)) { useless = false; break; }
     if (useless) { ++nb_useless_; return; }
     Rep& r = repairs_.emplace(id, Rep{id, std::move(ids), esz, bytes(), symsz, {}}).first->second;
-    if (batch_) r.expr.push_back(Term{std::make_shared<const bytes>(sym, sym + symsz), 1, symsz});
+    if (batch_) r.red.push_back(Term{base_node(sym, symsz), 1, symsz});
     else r.sym.assign(sym, sym + symsz);
     if (r.sym.empty()) r.sym.resize(1);
     std::vector<const Src*> known;
@@ -958,11 +1249,17 @@ class Decoder {
         const uint32_t c = inv[s * n + q];
         if (c) sizes[s] = static_cast<uint16_t>(f_.msize(reps[q]->esz, c) ^ sizes[s]);
       }
-    if (batch_) {                      // expressions; evaluated at the batch's flush
+    if (batch_) {                      // derived payloads, evaluated at the batch's flush
+      std::vector<NodeRef> rn(n);
+      for (size_t q = 0; q < n; ++q) rn[q] = repair_node(*reps[q]);
       for (size_t s = 0; s < n; ++s) {
-        Src src{mids[s], bytes(1, 0), sizes[s], {}};
-        for (size_t q = 0; q < n; ++q)
-          add_scaled(src.expr, reps[q]->expr, inv[s * n + q], std::min(sizes[s], reps[q]->symsz));
+        Expr e;
+        for (size_t q = 0; q < n; ++q) {
+          const uint32_t c = inv[s * n + q];
+          const uint16_t len = std::min(sizes[s], reps[q]->symsz);
+          if (c && len) e.push_back(Term{rn[q], c, len});
+        }
+        Src src{mids[s], bytes(1, 0), sizes[s], derived_node(f_.w, sizes[s], std::move(e))};
         insert_decoded(std::move(src));
       }
       nb_decoded_ += n;
@@ -1052,43 +1349,6 @@ class Batch {
   void flush();
 
  private:
-  // every pending expression of field w: one [n][kmax][stride] combine
-  void compute(uint32_t w)
-  {
-    std::vector<Pending*> jobs;
-    size_t kmax = 0, mx = 16;
-    for (Pending& p : q_) {
-      if (!p.eval || p.w != w) continue;
-      jobs.push_back(&p);
-      kmax = std::max(kmax, p.expr.size());
-      mx = std::max<size_t>(mx, p.size);
-      for (const Term& t : p.expr) mx = std::max<size_t>(mx, t.len);
-    }
-    if (jobs.empty()) return;
-    kmax = std::max<size_t>(kmax, 1);
-    const size_t stride = (mx + 15) / 16 * 16;
-    Device::get().combine_generations(w, jobs.size(), kmax, stride, [&](size_t g, size_t i,
-                                                                        const uint8_t** ptr,
-                                                                        uint16_t* len, uint32_t* c) {
-      const Pending& p = *jobs[g];
-      if (i >= p.expr.size()) return false;
-      *ptr = p.expr[i].base->data();
-      *len = p.expr[i].len;
-      *c = p.expr[i].c;
-      return true;
-    }, [&](size_t g, const uint8_t* sym) {
-      Pending& p = *jobs[g];
-      if (p.kind == Pending::ENC_PACKET) {
-        std::memcpy(p.pkt.data() + p.off1, sym, p.size);
-        std::memcpy(p.pkt.data() + p.off2, sym, p.size);
-      } else {
-        p.pkt.assign(sym, sym + p.size);
-      }
-      p.eval = false;                   // computed (a failed flush can be retried)
-      p.expr.clear();                   // release the payload snapshot
-    });
-  }
-
   std::vector<Encoder*> encs_;
   std::vector<Decoder*> decs_;
   std::vector<Pending> q_;
@@ -1129,20 +1389,38 @@ void Decoder::set_batch(Batch* b)
     batch_->detach(this);
   }
   if (!b) {
-    // back to immediate mode: materialise the symbols the protocol state still holds
-    std::vector<std::pair<Expr*, bytes*>> todo;
-    std::vector<uint16_t> lens;
-    for (auto& kv : sources_) { todo.push_back({&kv.second.expr, &kv.second.sym}); lens.push_back(kv.second.size); }
-    for (auto& kv : repairs_) { todo.push_back({&kv.second.expr, &kv.second.sym}); lens.push_back(kv.second.symsz); }
-    materialise(todo, lens);
+    // back to immediate mode: the payloads the protocol state still holds become host bytes
+    std::vector<NodeRef> rn;
+    std::vector<Node*> roots;
+    for (auto& kv : sources_)
+      if (kv.second.node) roots.push_back(kv.second.node.get());
+    for (auto& kv : repairs_) {
+      rn.push_back(repair_node(kv.second));
+      roots.push_back(rn.back().get());
+    }
+    if (!roots.empty()) Device::get().evaluate(roots);
+    auto host_bytes = [](const Node& n, uint16_t size) {
+      bytes v(n.host.begin(), n.host.begin() + std::min<size_t>(n.host.size(), size));
+      v.resize(std::max<size_t>(size, 1), 0);
+      return v;
+    };
+    for (auto& kv : sources_)
+      if (kv.second.node) {
+        kv.second.sym = host_bytes(*kv.second.node, kv.second.size);
+        kv.second.node.reset();
+      }
+    size_t i = 0;
+    for (auto& kv : repairs_) {
+      kv.second.sym = host_bytes(*rn[i++], kv.second.symsz);
+      kv.second.red.clear();
+    }
   } else {
     // into batch mode: the held symbols become base payloads
     for (auto& kv : sources_)
-      if (kv.second.expr.empty() && kv.second.size)
-        kv.second.expr.push_back(Term{std::make_shared<const bytes>(kv.second.sym.begin(), kv.second.sym.begin() + kv.second.size), 1, kv.second.size});
+      if (!kv.second.node) kv.second.node = base_node(kv.second.sym.data(), kv.second.size);
     for (auto& kv : repairs_)
-      if (kv.second.expr.empty() && kv.second.symsz)
-        kv.second.expr.push_back(Term{std::make_shared<const bytes>(kv.second.sym.begin(), kv.second.sym.begin() + kv.second.symsz), 1, kv.second.symsz});
+      if (kv.second.red.empty())
+        kv.second.red.push_back(Term{base_node(kv.second.sym.data(), kv.second.symsz), 1, kv.second.symsz});
   }
   batch_ = b;
   if (b) b->attach(this);
@@ -1161,14 +1439,25 @@ Batch::~Batch()
 
 void Batch::flush()
 {
-  for (uint32_t w : {4u, 8u, 16u, 32u}) compute(w);
+  // every payload the queued events emit: evaluated (with what it reads) and fetched, all fields
+  // and objects of the batch together
+  std::vector<Node*> roots;
+  for (const Pending& p : q_)
+    if (p.node && !p.node->has_value()) roots.push_back(p.node.get());
+  if (!roots.empty()) Device::get().evaluate(roots);
   std::vector<Pending> q;
   q.swap(q_);
-  for (const Pending& p : q) {
+  for (Pending& p : q) {
     if (p.kind == Pending::DEC_DATA) {
       const ntc_data_handler& h = p.dec->data_handler();
-      h.read_data(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.size);
+      static const uint8_t zero[16] = {0};
+      const uint8_t* d = p.size ? p.node->host.data() : zero;
+      h.read_data(h.context, reinterpret_cast<const char*>(d), p.size);
       continue;
+    }
+    if (p.node) {                        // encoder repair: both copies of the symbol
+      std::memcpy(p.pkt.data() + p.off1, p.node->host.data(), p.size);
+      std::memcpy(p.pkt.data() + p.off2, p.node->host.data(), p.size);
     }
     const ntc_packet_handler& h = p.kind == Pending::ENC_PACKET ? p.enc->handler()
                                                                 : p.dec->packet_handler();

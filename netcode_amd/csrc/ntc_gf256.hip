@@ -1900,6 +1900,42 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 }
 
 // ----------------------------------------------------------------------- region multiply ----
+// ntc_gf256_gather_combine: one wave per (job, 1 KiB of its output); a lane owns 16 bytes.  The
+// terms of a job are wave-uniform: their descriptors and the v_perm tables of their coefficients
+// come through the scalar cache.
+__global__ __launch_bounds__(64) void gather_combine(const ntc_gf256_gather_job* __restrict__ jobs,
+                                                     const ntc_gf256_gather_term* __restrict__ terms)
+{
+  static_assert(sizeof(ntc_gf256_gather_job) == 24 && sizeof(ntc_gf256_gather_term) == 16, "layout");
+  const u32x4 j4 = const_load<u32x4>(jobs + blockIdx.x);           // out (2 dwords), term0, nterms
+  const uint32_t jlen = const_load<uint32_t>(reinterpret_cast<const uint8_t*>(jobs + blockIdx.x) + 16);
+  uint8_t* out = reinterpret_cast<uint8_t*>((static_cast<uint64_t>(j4[1]) << 32) | j4[0]);
+  const uint32_t col = blockIdx.y * 1024u + threadIdx.x * 16u;
+  if (col >= ((jlen + 15u) & ~15u)) return;
+  uint32_t acc[4] = {0, 0, 0, 0};
+  for (uint32_t t = 0; t < j4[3]; ++t) {
+    const u32x4 t4 = const_load<u32x4>(terms + j4[2] + t);          // src (2 dwords), len, coef
+    const uint32_t tlen = t4[2];
+    if (col >= tlen) continue;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(t4[1]) << 32) | t4[0]);
+    const uint4 v = *reinterpret_cast<const uint4*>(src + col);
+    uint32_t x[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t rem = tlen - col;                   // bytes of this piece that take part
+    if (rem < 16u) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t keep = rem > 4u * d ? rem - 4u * d : 0u;
+        x[d] &= keep >= 4u ? 0xFFFFFFFFu : (1u << (8u * keep)) - 1u;
+      }
+    }
+    const uint32_t* tb = d_perm.w[t4[3] & 0xFFu];
+    const uint32_t tf[5] = {tb[0], tb[1], tb[2], tb[3], tb[4]};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[d] ^= mul4(tf, x[d]);
+  }
+  *reinterpret_cast<uint4*>(out + col) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+}
+
 __global__ __launch_bounds__(256) void region_mul(const uint8_t* __restrict__ src,
                                                   uint8_t* __restrict__ dst, size_t len,
                                                   uint32_t c, int add)
@@ -2442,6 +2478,18 @@ int ntc_gf256_combine_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_
   a.G = G; a.k = k; a.rows = rows; a.stride = stride;
   a.in0 = in; a.out = out; a.coef = coef; a.rp = tile_rp(rows);
   return launch_mac(e, false, a, static_cast<hipStream_t>(stream), "combine launch");
+}
+
+int ntc_gf256_gather_combine(ntc_gf256_engine* e, uint32_t njobs, const ntc_gf256_gather_job* jobs,
+                             const ntc_gf256_gather_term* terms, uint32_t max_len, void* stream)
+{
+  if (!e || (njobs && (!jobs || !terms))) return fail(NTC_GPU_EINVAL, "NULL argument");
+  if (njobs == 0 || max_len == 0) return NTC_GPU_OK;
+  if (max_len > 65535) return fail(NTC_GPU_EUNSUPPORTED, "gather_combine: payloads up to 65535 bytes");
+  (void)hipSetDevice(e->device);
+  hipLaunchKernelGGL(gather_combine, dim3(njobs, (max_len + 1023) / 1024), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), jobs, terms);
+  return hip_check(hipGetLastError(), "gather_combine launch");
 }
 
 int ntc_gf256_region_multiply(ntc_gf256_engine* e, const uint8_t* src, uint8_t* dst, size_t len,

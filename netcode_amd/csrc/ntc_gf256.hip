@@ -730,16 +730,40 @@ struct PrepArgs {
   uint16_t* rep_len;
 };
 
+// Coefficients of one repair row along sources i, i + step, ... without multiplies:
+// P = (R1 + S1) * R1 mod 2^32 grows by D = step * R1 per step, and since 2^32 = 1 (mod 255) the
+// residue p = P mod 255 follows as p + (D mod 255) - carry(P + D).  coefficient = p + 1
+// (galois_field.hh:143-158).
+struct CoefWalk {
+  uint32_t P, p, D, d;
+  __device__ __forceinline__ CoefWalk(uint32_t R1, uint32_t S1, uint32_t step)
+      : P((R1 + S1) * R1), D(step * R1)
+  {
+    p = P % 255u;
+    d = D % 255u;
+  }
+  __device__ __forceinline__ uint32_t coef() const { return p + 1u; }
+  __device__ __forceinline__ void next()
+  {
+    const uint32_t nP = P + D;
+    const uint32_t t = p + d + (nP < P ? 254u : 255u);   // in [254, 763]
+    const uint32_t t1 = min(t, t - 255u);
+    p = min(t1, t1 - 255u);
+    P = nP;
+  }
+};
+
+// One wave per generation, four generations per 256-thread block (one LDS table copy for the
+// four).  Lane = (coefficient word w of a source row = rows 4w..4w+3, source slot q): the lane
+// walks sources q, q + nq, ..., writes its coefficient words and XORs the coded lengths of its
+// sources into the four rows' encoded sizes; the slots' partial sizes are reduced through the
+// wave's LDS slice.  No block-wide barrier after the table copy.
 __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
 {
-  const uint32_t g = blockIdx.x;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
-  // LDS copy of the v_perm tables (encoded sizes).  Small generations (k * r < 1024: under 4
-  // size lookups per thread) read the tables from the constant bank instead: cheaper than an
-  // 8 KiB copy and a barrier per block (k=32 r=8: 0.0115 -> 0.0100 ms per batch; k=128 r=32
-  // keeps the copy: 0.030 vs 0.043 ms without it)
+  // LDS copy of the v_perm tables (encoded sizes).  Small generations (k * r < 1024) read the
+  // tables from the constant bank instead.
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
+  __shared__ uint16_t part[4][256];
   const bool lds_tabs = a.k * a.r >= 1024u;
   if (lds_tabs) {                                 // uniform
     const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
@@ -748,49 +772,65 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
     __syncthreads();
   }
   const uint32_t (*tabs)[8] = lds_tabs ? ptab : d_perm.w;
-  {
-    uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp;
-    const uint32_t n = a.k * a.rp;
-    for (uint32_t t = threadIdx.x * 4; t < n; t += 256 * 4) {
-      uint32_t w = 0;
-#pragma unroll
-      for (uint32_t b = 0; b < 4; ++b) {
-        const uint32_t i = (t + b) / a.rp, j = (t + b) % a.rp;
-        if (j < a.r) w |= coefficient(ridb + j, sidb + i) << (8 * b);
-      }
-      *reinterpret_cast<uint32_t*>(coef + t) = w;   // rp is a multiple of 4
-    }
-  }
-  // encoded sizes: the k sources of a repair split over 256 / r thread segments, XOR-reduced
-  __shared__ uint16_t part[256];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 4u + wv;
+  if (g >= a.G) return;
+  const uint32_t nw = a.rp >> 2;                  // rp % 4 == 0, rp <= 256: nw <= 64
+  const uint32_t nq = 64u / nw;                   // source slots
+  const uint32_t w = lane % nw, q = lane / nw;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
   const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
-  const uint32_t segs = a.r >= 256 ? 1u : 256u / a.r;
-  for (uint32_t j0 = 0; j0 < a.r; j0 += 256) {
-    const uint32_t rows = min(256u, a.r - j0);
-    const uint32_t sg = rows >= 256 ? 1u : segs;
-    uint16_t esz = 0;
-    if (threadIdx.x < rows * sg) {
-      const uint32_t j = j0 + threadIdx.x % rows, seg = threadIdx.x / rows;
-      // both length bytes times c in one v_perm lookup (galois_field.hh:108-115 codes a u16 as
-      // a 2-byte region; a zero length stays zero)
-      for (uint32_t i = seg; i < a.k; i += sg)
-        esz ^= static_cast<uint16_t>(mul4(tabs[coefficient(ridb + j, sidb + i)], len[i]));
-    }
-    part[threadIdx.x] = esz;
-    __syncthreads();
-    if (threadIdx.x < rows) {
-      uint16_t e = 0;
-      for (uint32_t q = 0; q < sg; ++q) e ^= part[q * rows + threadIdx.x];
-      a.rep_size[static_cast<size_t>(g) * a.r + j0 + threadIdx.x] = e;
-    }
-    __syncthreads();
-  }
-  if (a.rep_len && threadIdx.x < 64) {
-    uint32_t mx = 0;
-    for (uint32_t t = threadIdx.x; t < a.k; t += 64) mx = max(mx, static_cast<uint32_t>(len[t]));
+  uint16_t* pw = part[wv];
+  uint32_t lmax = 0;
+  if (q < nq) {
+    uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp + 4u * w;
+    CoefWalk cw[4] = {CoefWalk(ridb + 4u * w + 1u, sidb + q + 1u, nq),
+                      CoefWalk(ridb + 4u * w + 2u, sidb + q + 1u, nq),
+                      CoefWalk(ridb + 4u * w + 3u, sidb + q + 1u, nq),
+                      CoefWalk(ridb + 4u * w + 4u, sidb + q + 1u, nq)};
+    uint32_t esz[4] = {0, 0, 0, 0};
+    // four sources per pass, their lengths loaded together (one memory round trip per 4)
+    for (uint32_t ib = q; ib < a.k; ib += 4u * nq) {
+      uint32_t lq[4];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, o)));
-    if (threadIdx.x == 0) a.rep_len[g] = static_cast<uint16_t>(mx);
+      for (uint32_t e = 0; e < 4; ++e) lq[e] = ib + e * nq < a.k ? len[ib + e * nq] : 0u;
+#pragma unroll
+      for (uint32_t e = 0; e < 4; ++e) {
+        const uint32_t i = ib + e * nq;
+        if (i >= a.k) break;
+        lmax = max(lmax, lq[e]);
+        uint32_t word = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+          if (4u * w + b < a.r) {                 // rows >= r stay zero
+            const uint32_t c = cw[b].coef();
+            word |= c << (8 * b);
+            // both length bytes times c in one v_perm lookup (galois_field.hh:108-115 codes a
+            // u16 as a 2-byte region; a zero length stays zero)
+            esz[b] ^= mul4(tabs[c], lq[e]);
+          }
+          cw[b].next();
+        }
+        *reinterpret_cast<uint32_t*>(coef + static_cast<size_t>(i) * a.rp) = word;
+      }
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) pw[q * a.rp + 4u * w + b] = static_cast<uint16_t>(esz[b]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // pw holds nq * rp <= 256 partial sizes
+  for (uint32_t j = lane; j < a.r; j += 64u) {
+    uint16_t e = 0;
+    for (uint32_t s2 = 0; s2 < nq; ++s2) e ^= pw[s2 * a.rp + j];
+    a.rep_size[static_cast<size_t>(g) * a.r + j] = e;
+  }
+  if (a.rep_len) {                                // repair length = max source length
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, static_cast<uint32_t>(__shfl_xor(lmax, o)));
+    if (lane == 0) a.rep_len[g] = static_cast<uint16_t>(lmax);
   }
 }
 
@@ -2328,7 +2368,7 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   p.coef = static_cast<uint8_t*>(e->enc_coef);
   {
     KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st, true);
-    hipExtLaunchKernelGGL(encode_prep, dim3(G), dim3(256), 0, st, kt.start(), kt.stop(), 0, p);
+    hipExtLaunchKernelGGL(encode_prep, dim3((G + 3) / 4), dim3(256), 0, st, kt.start(), kt.stop(), 0, p);
   }
   if ((rc = hip_check(hipGetLastError(), "encode_prep launch"))) return rc;
   MacArgs a{};

@@ -21,6 +21,10 @@ struct ntc_gf256_engine {
   uint8_t* plan_coef = nullptr;
   void* enc_coef = nullptr;
   size_t enc_coef_cap = 0;
+  // encode generation pairing (short symbols, continuous ids): per generation 0 = alone,
+  // 1 = shares its MAC wave with generation g + 255 (equal coefficient matrices), 2 = that partner
+  void* enc_pair = nullptr;
+  size_t enc_pair_cap = 0;
   // the last plan also wrote the decode MAC's input row addresses (row_ptr) for these buffers
   const uint8_t* rows_src = nullptr;
   const uint8_t* rows_rep = nullptr;

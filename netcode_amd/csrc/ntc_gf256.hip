@@ -166,6 +166,8 @@ struct MacArgs {
   const uint64_t* row_ptr;     // bit-sliced decode: input row address per plan position,
                                // [G][k + kBsRing] (plan_rows; the tail repeats position k-1)
   uint32_t tile_fast;          // bit-sliced task order: 1 = row tile fastest, 0 = column span fastest
+  const uint8_t* pair;         // encode pairing flags [G] (gf_mac_bs<.., PAIR>), see kPairGap
+  uint64_t pair_in, pair_out;  // byte distance of the partner's sources / repairs
 };
 
 // ---- hand-scheduled scalar loads -------------------------------------------------------------
@@ -451,12 +453,16 @@ template <> struct BsCoef<16> { using T = u32x4; };
 // SIMD); its source is read from LDS at the top of its own iteration (no register copy of the
 // next one).  FULL: the span lies inside the stride (stride % 2048 == 0), so both pieces come
 // from one lane offset; else each piece has its own, clamped to the span's first bytes when it
-// lies past the stride (loaded, never stored).
-template <int R, bool DEC, bool FULL>
+// lies past the stride (loaded, never stored).  PAIR (encode, stride <= 1024): the second piece
+// of each lane holds the same bytes of the partner generation (poff_in / poff_out bytes further
+// on; 0 and never stored when the generation is alone).
+template <int R, bool DEC, bool FULL, bool PAIR = false>
 __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t tile,
-                                        uint32_t nrows, uint32_t cc, uint32_t lane, uint32_t ring)
+                                        uint32_t nrows, uint32_t cc, uint32_t lane, uint32_t ring,
+                                        uint64_t poff_in = 0, uint64_t poff_out = 0)
 {
   static_assert(R == 8 || R == 16, "8- or 16-row tiles");
+  static_assert(!PAIR || (!DEC && !FULL), "pairing is an encode mode for short symbols");
   static_assert(kBsRing == 4, "the unrolled loop assumes a 4-slot ring");
   constexpr bool kLate = R == 16;
   using CoefV = typename BsCoef<R>::T;
@@ -467,8 +473,8 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   // scalar row base is pre-biased by col - ring.
   const uint32_t x = ring + lane * 16u;
   const bool v0 = FULL || col + lane * 16u < stride;
-  const bool v1 = FULL || col + lane * 16u + 1024u < stride;
-  const uint32_t d0 = v0 ? x : ring, d1 = v1 ? x + 1024u : ring;   // !FULL DMA offsets
+  const bool v1 = PAIR ? poff_out != 0 && v0 : FULL || col + lane * 16u + 1024u < stride;
+  const uint32_t d0 = v0 ? x : ring, d1 = v1 ? (PAIR ? x : x + 1024u) : ring;   // !FULL DMA offsets
   const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
   const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
   const uint32_t jstep = a.rp;
@@ -500,9 +506,10 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
                    "global_load_lds_dwordx4 %1, %3\n\t"
                    "s_add_u32 m0, %4, 0x400\n\ts_nop 0\n\t"
-                   "global_load_lds_dwordx4 %2, %3\n\t"
+                   "global_load_lds_dwordx4 %2, %5\n\t"
                    "s_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(d0), "v"(d1), "s"(row), "s"(slot) : "memory", "scc");
+                   : "=&s"(keep) : "v"(d0), "v"(d1), "s"(row), "s"(slot), "s"(row + (PAIR ? poff_in : 0))
+                   : "memory", "scc");
   };
 
   u32x8 A[R];
@@ -549,6 +556,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       // iteration ago, and this block's LDS wait already covered it); then the next refill's row
       // address, loaded before the chain so its latency hides behind it
       const uint8_t* row = nrow + bias;
+      const uint8_t* row2 = PAIR ? row + poff_in : row;   // the second piece's row (pairing)
       const uint8_t* nrow_next = DEC ? row_at(i + kBsRing) : nrow + ((i + kBsRing < k) ? stride : 0u);
       // refill the slot of source i-1 with source i+3, then the chain (one M0 save / restore)
 #define NTC_BS_DMA_FULL \
@@ -557,7 +565,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
 #define NTC_BS_DMA_PART \
       "s_mov_b32 s94, m0\n" "s_mov_b32 m0, %[slot]\n" "s_nop 0\n" \
       "global_load_lds_dwordx4 %[d0], %[row]\n" "s_add_u32 m0, %[slot], 0x400\n" "s_nop 0\n" \
-      "global_load_lds_dwordx4 %[d1], %[row]\n"
+      "global_load_lds_dwordx4 %[d1], %[row2]\n"
 #define NTC_BS_ENTER \
       "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n" \
       "s_lshl_b32 s98, s90, 24\n" "s_lshr_b32 s98, s98, 17\n" \
@@ -582,7 +590,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
           asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_LEAVE
                        : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
-                         [d1] "v"(d1), [row] "s"(row)
+                         [d1] "v"(d1), [row] "s"(row), [row2] "s"(row2)
                        : NTC_BS_CLOB);
       } else {
         const uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];
@@ -596,7 +604,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
           asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
                        : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
-                         [d1] "v"(d1), [row] "s"(row), [p1] "s"(P1)
+                         [d1] "v"(d1), [row] "s"(row), [row2] "s"(row2), [p1] "s"(P1)
                        : NTC_BS_CLOB);
       }
       nrow = nrow_next;
@@ -621,14 +629,14 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
     }
     if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-    if (v1) *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+    if (v1) *reinterpret_cast<uint4*>(dst + (PAIR ? poff_out + c0 : c1)) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
   }
 }
 
 // One wave per (generation, R-row tile, 2 KiB column span).  Blocks are renumbered so that each
 // XCD (block b runs on XCD b % 8) owns a contiguous range of tasks: the row tiles of one
 // generation then share that XCD's L2 instead of each pulling the sources from HBM.
-template <int R, bool DEC, bool FULL>
+template <int R, bool DEC, bool FULL, bool PAIR = false>
 __global__ __launch_bounds__(64 * kBsWaves)
 __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
 {
@@ -659,7 +667,13 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
   if (row0 >= total) return;
   const uint32_t nrows = min(static_cast<uint32_t>(R), total - row0);
   const uint32_t ring = lds_addr(s_ring + wave * (kBsRing * kBsSlot));
-  bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring);
+  if constexpr (PAIR) {
+    const uint32_t pf = uniform(static_cast<uint32_t>(a.pair[g]));
+    if (pf == 2) return;                               // encoded by its partner's wave
+    bs_tile<R, DEC, FULL, true>(a, g, tile, nrows, cc, lane, ring, pf ? a.pair_in : 0, pf ? a.pair_out : 0);
+  } else {
+    bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring);
+  }
 }
 
 // Input row address of every plan position for the bit-sliced decode MAC: position i < k reads
@@ -728,7 +742,16 @@ struct PrepArgs {
   uint8_t* coef;
   uint16_t* rep_size;
   uint16_t* rep_len;
+  uint8_t* pair;               // non-null: try to pair generation g with g + kPairGap
 };
+
+// Generation pairing for the encode MAC (symbols of at most half a bit-sliced span): with
+// continuous ids (sid = g*k + i, rid = g*r + j) the coefficient of generation g + 255 is that of g
+// unless the uint32 product wraps a different number of times (galois_field.hh:143-158; 2^32 = 1
+// mod 255), so most generations g with (g / 255) even share their matrix with g + 255.  encode_prep
+// compares the two matrices; equal ones are encoded by one MAC wave, g's symbols in the first
+// half of each lane's span and the partner's in the second.
+constexpr uint32_t kPairGap = 255;
 
 // Coefficients of one repair row along sources i, i + step, ... without multiplies:
 // P = (R1 + S1) * R1 mod 2^32 grows by D = step * R1 per step, and since 2^32 = 1 (mod 255) the
@@ -783,12 +806,26 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
   const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
   uint16_t* pw = part[wv];
   uint32_t lmax = 0;
+  // pairing: a first-of-pair generation also walks its partner's coefficients and compares them
+  // (only when the partner's id bases are congruent mod 255, the necessary condition)
+  const bool first = a.pair && (g / kPairGap) % 2u == 0u;
+  const bool has_partner = first && g + kPairGap < a.G;
+  uint32_t psidb = 0, pridb = 0;
+  if (has_partner) {
+    const uint32_t gp = g + kPairGap;
+    psidb = a.sid_base ? a.sid_base[gp] : gp * a.k;
+    pridb = a.rid_base ? a.rid_base[gp] : gp * a.r;
+  }
+  const bool cmp = has_partner && psidb % 255u == sidb % 255u && pridb % 255u == ridb % 255u;
+  uint32_t diff = 0;
   if (q < nq) {
     uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp + 4u * w;
     CoefWalk cw[4] = {CoefWalk(ridb + 4u * w + 1u, sidb + q + 1u, nq),
                       CoefWalk(ridb + 4u * w + 2u, sidb + q + 1u, nq),
                       CoefWalk(ridb + 4u * w + 3u, sidb + q + 1u, nq),
                       CoefWalk(ridb + 4u * w + 4u, sidb + q + 1u, nq)};
+    CoefWalk cp[4] = {CoefWalk(pridb + 4u * w + 1u, psidb + q + 1u, nq), CoefWalk(pridb + 4u * w + 2u, psidb + q + 1u, nq),
+                      CoefWalk(pridb + 4u * w + 3u, psidb + q + 1u, nq), CoefWalk(pridb + 4u * w + 4u, psidb + q + 1u, nq)};
     uint32_t esz[4] = {0, 0, 0, 0};
     // four sources per pass, their lengths loaded together (one memory round trip per 4)
     for (uint32_t ib = q; ib < a.k; ib += 4u * nq) {
@@ -800,7 +837,7 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
         const uint32_t i = ib + e * nq;
         if (i >= a.k) break;
         lmax = max(lmax, lq[e]);
-        uint32_t word = 0;
+        uint32_t word = 0, pword = 0;
 #pragma unroll
         for (uint32_t b = 0; b < 4; ++b) {
           if (4u * w + b < a.r) {                 // rows >= r stay zero
@@ -809,14 +846,24 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
             // both length bytes times c in one v_perm lookup (galois_field.hh:108-115 codes a
             // u16 as a 2-byte region; a zero length stays zero)
             esz[b] ^= mul4(tabs[c], lq[e]);
+            if (cmp) pword |= cp[b].coef() << (8 * b);
           }
           cw[b].next();
+          if (cmp) cp[b].next();
         }
+        diff |= word ^ pword;
         *reinterpret_cast<uint32_t*>(coef + static_cast<size_t>(i) * a.rp) = word;
       }
     }
 #pragma unroll
     for (uint32_t b = 0; b < 4; ++b) pw[q * a.rp + 4u * w + b] = static_cast<uint16_t>(esz[b]);
+  }
+  if (first) {
+    const bool same = cmp && __ballot(diff != 0) == 0;
+    if (lane == 0) {
+      a.pair[g] = same ? 1 : 0;
+      if (has_partner) a.pair[g + kPairGap] = same ? 2 : 0;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -2058,9 +2105,10 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
   return pieces * 100 >= spans * 128 * 33;
 }
 
-// Bit-sliced MAC kernel for a tile height and span shape.
-mac_fn pick_bs(bool dec, uint32_t rowtile, bool full)
+// Bit-sliced MAC kernel for a tile height and span shape (pair: the encode pairing form).
+mac_fn pick_bs(bool dec, uint32_t rowtile, bool full, bool pair)
 {
+  if (pair) return rowtile == 16 ? gf_mac_bs<16, false, false, true> : gf_mac_bs<8, false, false, true>;
   if (rowtile == 16)
     return dec ? (full ? gf_mac_bs<16, true, true> : gf_mac_bs<16, true, false>)
                : (full ? gf_mac_bs<16, false, true> : gf_mac_bs<16, false, false>);
@@ -2074,14 +2122,14 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   mac_fn fn;
   uint32_t rowtile, span, wpb;
   uint64_t blk_align = 1;
-  if (use_bitslice(e, a.stride)) {
+  if (a.pair || use_bitslice(e, a.stride)) {
     // 16-row tiles (3 waves per SIMD) once a tile has more than 8 rows to fill, else 8-row
     // tiles (4 waves per SIMD)
     rowtile = a.rows > 8 ? 16u : 8u;
     span = 2048;
     wpb = kBsWaves;
     blk_align = 8;                              // the kernel's XCD renumbering
-    fn = pick_bs(dec, rowtile, a.stride % 2048 == 0);
+    fn = pick_bs(dec, rowtile, a.stride % 2048 == 0, a.pair != nullptr);
     if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBsRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
@@ -2237,6 +2285,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_out);
   (void)hipFree(e->plan_coef);
   (void)hipFree(e->enc_coef);
+  (void)hipFree(e->enc_pair);
   (void)hipFree(e->row_ptr);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   for (auto& pair : e->mac_ev)
@@ -2341,6 +2390,7 @@ int ntc_gf256_reserve(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r)
   const uint32_t rp = tile_rp(r);
   int rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   if (rc) return rc;
+  if ((rc = ensure_buf(&e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair"))) return rc;
   // the decode MAC's input row addresses (decode_plan_w / plan_rows), so later calls never allocate
   if ((rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<size_t>(G) * (k + kBsRing) * 8,
                        "hipMalloc row_ptr")))
@@ -2362,10 +2412,19 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   hipStream_t st = static_cast<hipStream_t>(stream);
   rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   if (rc) return rc;
+  // generation pairing (kPairGap): symbols of at most half a bit-sliced span that fill at least a
+  // third of it when paired; pays off with continuous ids
+  const bool pairing = G > kPairGap && stride <= 1024 &&
+                       (e->mac_kind == NTC_GF256_MAC_BITSLICE ||
+                        (e->mac_kind == NTC_GF256_MAC_AUTO && 2u * stride * 100u >= 2048u * 33u));
+  if (pairing &&
+      (rc = ensure_buf(&e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair")))
+    return rc;
   PrepArgs p{};
   p.G = G; p.k = k; p.r = r; p.rp = rp; p.src_len = src_len; p.sid_base = sid_base;
   p.rid_base = rid_base; p.rep_size = rep_size; p.rep_len = rep_len;
   p.coef = static_cast<uint8_t*>(e->enc_coef);
+  p.pair = pairing ? static_cast<uint8_t*>(e->enc_pair) : nullptr;
   {
     KernelTimer kt(e, NTC_GF256_K_ENCODE_PREP, st, true);
     hipExtLaunchKernelGGL(encode_prep, dim3((G + 3) / 4), dim3(256), 0, st, kt.start(), kt.stop(), 0, p);
@@ -2374,6 +2433,9 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   MacArgs a{};
   a.G = G; a.k = k; a.rows = r; a.stride = stride;
   a.in0 = src; a.out = rep; a.coef = static_cast<const uint8_t*>(e->enc_coef); a.rp = rp;
+  a.pair = p.pair;
+  a.pair_in = static_cast<uint64_t>(kPairGap) * k * stride;
+  a.pair_out = static_cast<uint64_t>(kPairGap) * r * stride;
   return launch_mac(e, false, a, st, "encode_mac launch");
 }
 

@@ -94,6 +94,15 @@ ENCODE_CASES = [
     # lean-loop MAC (full 2 KiB spans, k % 4 == 0): only the final group of 4 sources; 3 spans
     (5, 4, 3, 2048, 2048, True, "offset"),
     (3, 12, 9, 6144, 6144, True, "wrap"),
+    # generation pairing (continuous ids, stride <= 1024, G > 255): g and g + 255 share one MAC
+    # wave when their matrices match; a tail of unpaired generations; odd row tiles; half fill
+    (700, 32, 8, 1024, 1024, True, "default"),
+    (600, 16, 4, 512, 512, True, "default"),
+    (520, 9, 20, 688, 688, True, "default"),
+    (600, 16, 4, 1024, 1024, False, "offset"),        # explicit continuous bases
+    (600, 16, 4, 1024, 1024, False, "wrap"),          # explicit bases whose products wrap
+    # config 2 itself: uint32 wraps make some g / g + 255 matrices differ (those stay unpaired)
+    (4096, 32, 8, 1024, 1024, False, "default"),
 ]
 
 

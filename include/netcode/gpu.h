@@ -150,20 +150,24 @@ int  ntc_gf256_combine_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint
 /* Gathered combination over payloads that already live on the device (the per-packet batching
  * adaptor's resident payload arena, netcode/c/ext.h ntc_batch_*):
  *   out_j[0 .. len_j) = sum_{t in job j} coef_t * src_t[0 .. len_t)   (src zero-extended past len_t)
- * jobs [njobs] and terms (indexed by the jobs) are device arrays; every src / out address is
- * 16-byte aligned with readable / writable bytes up to len rounded up to 16 (outputs are zero-
- * padded there); len_t <= len_j; max_len >= every len_j.  One wave per (job, 1 KiB of output).
+ * and, when out2_j != 0, the same bytes at out2_j too.  jobs [njobs] and terms (indexed by the
+ * jobs) are device arrays; src / out / out2 are device addresses or pinned host memory
+ * (hipHostMalloc: the adaptor reads this flush's new payloads and writes the results it hands to
+ * callbacks there, with no copy engine in between), 16-byte aligned with readable / writable
+ * bytes up to len rounded up to 16 (outputs are zero-padded there); len_t <= len_j;
+ * max_len >= every len_j.  One wave per (job, 1 KiB of output).
  * Replaces, for a whole batch flush, the per-operation region calls of detail/encoder.cc:15-64
  * and detail/decoder.cc:156-178, 393-408, 503-534. */
 typedef struct {
-  uint64_t out;          /* device address of the output payload */
+  uint64_t out;          /* address of the output payload */
+  uint64_t out2;         /* 0, or a second address receiving the same bytes */
   uint32_t term0;        /* first term of this job */
   uint32_t nterms;
   uint32_t len;          /* output bytes (<= 65535) */
   uint32_t pad;
 } ntc_gf256_gather_job;
 typedef struct {
-  uint64_t src;          /* device address of an input payload */
+  uint64_t src;          /* address of an input payload */
   uint32_t len;          /* bytes of it that take part */
   uint32_t coef;         /* GF(2^8) coefficient (low byte) */
 } ntc_gf256_gather_term;

@@ -73,6 +73,7 @@ struct DevChunk {
 
 struct Node;
 using NodeRef = std::shared_ptr<Node>;
+constexpr uint32_t kNoPos = ~0u;
 // c * (the first len bytes of node's payload, zero-extended)
 struct Term {
   NodeRef node;
@@ -84,7 +85,8 @@ using Expr = std::vector<Term>;
 // A payload: base (bytes handed in or received) or derived (a linear combination of other
 // payloads, evaluated at a batch flush after everything it reads).  Immutable once created.
 struct Node {
-  bytes host;                  // base: the payload; derived: its value once fetched
+  bytes host;                  // base: the payload (from byte hoff on); derived: its value once fetched
+  uint32_t hoff = 0;           // a received packet's buffer is adopted whole: payload offset in it
   uint16_t size = 0;
   uint32_t w = 8;              // field of a derived node's coefficients
   bool derived = false;
@@ -95,17 +97,30 @@ struct Node {
   uint32_t off = 0;
   int level = 0;               // flush bookkeeping: evaluation level, visit stamp
   uint64_t mark = 0;
+  const uint8_t* stage = nullptr;   // during a flush: the pinned staged copy this flush uploads
+  uint32_t rpos = ~0u;         // during a flush: offset of the fetched value in the result staging
   ~Node()
   {
     if (chunk) chunk->live.fetch_sub(1, std::memory_order_relaxed);
   }
   bool has_value() const { return !derived || fetched; }
+  const uint8_t* data() const { return host.data() + hoff; }
 };
 
 inline NodeRef base_node(const uint8_t* p, size_t n)
 {
   auto nd = std::make_shared<Node>();
   nd->host.assign(p, p + n);
+  nd->size = static_cast<uint16_t>(n);
+  return nd;
+}
+
+// A base payload that takes over the buffer it lies in (a received packet): no copy.
+inline NodeRef adopt_node(bytes&& buf, size_t off, size_t n)
+{
+  auto nd = std::make_shared<Node>();
+  nd->host = std::move(buf);
+  nd->hoff = static_cast<uint32_t>(off);
   nd->size = static_cast<uint16_t>(n);
   return nd;
 }
@@ -287,7 +302,7 @@ class Device {
           [&](size_t g, size_t i, const uint8_t** ptr, uint16_t* len, uint32_t* c) {
             const Node* n = todo[a + g];
             if (i >= n->expr.size()) return false;
-            *ptr = n->expr[i].node->host.data();
+            *ptr = n->expr[i].node->data();
             *len = n->expr[i].len;
             *c = n->expr[i].c;
             return true;
@@ -329,9 +344,14 @@ class Device {
     return cur_;
   }
 
+  // One flush of GF(2^8) jobs.  The payloads the jobs read that are not on the device yet are
+  // staged in pinned host memory: the jobs of this flush read them from there, and copy jobs in
+  // the same launch store them into the arena for later flushes.  A root's result is written by
+  // its job both into the arena and straight into pinned host memory (the job's second output),
+  // so a flush is one descriptor copy, one launch per dependency level and one synchronisation.
   void evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep)
   {
-    // base payloads (and host-evaluated ones) the jobs read that are not on the device yet
+    const uint64_t up_mark = ep + (1ull << 63);
     std::vector<Node*> up;
     size_t up_bytes = 0, out_bytes = 0, nterms = 0;
     for (Node* n : todo) {
@@ -339,104 +359,111 @@ class Device {
       out_bytes += pad16(n->size);
       for (const Term& t : n->expr) {
         Node* c = t.node.get();
-        if (c->chunk || (c->derived && !c->done) || c->mark == ep + (1ull << 63)) continue;
-        c->mark = ep + (1ull << 63);
+        if (c->chunk || (c->derived && !c->done) || c->mark == up_mark) continue;
+        c->mark = up_mark;
         up.push_back(c);
         up_bytes += pad16(c->size);
       }
     }
-    // roots evaluated by an earlier flush (only on the device): fetched one by one below
+    // results the host needs: roots evaluated now (second output) and earlier (device copy)
+    size_t root_bytes = 0, late_bytes = 0;
     std::vector<Node*> late;
-    size_t late_bytes = 0;
-    for (Node* r : roots)
-      if (r->derived && r->done && !r->fetched && r->chunk) {
+    for (Node* r : roots) {
+      if (!r->derived || r->fetched) continue;
+      if (!r->done) {
+        r->rpos = static_cast<uint32_t>(root_bytes);
+        root_bytes += pad16(r->size);
+      } else if (r->chunk) {
         late.push_back(r);
         late_bytes += pad16(r->size);
       }
+    }
     if (todo.empty() && late.empty()) return;
     size_t base = 0;
     DevChunk* ch = (up_bytes + out_bytes) ? arena_alloc(up_bytes + out_bytes, &base) : nullptr;
-    grow_stage(up_bytes, out_bytes + late_bytes,
-               todo.size() * sizeof(ntc_gf256_gather_job) + nterms * sizeof(ntc_gf256_gather_term));
+    const size_t njobs = up.size() + todo.size();
+    grow_stage(up_bytes, root_bytes + late_bytes,
+               njobs * sizeof(ntc_gf256_gather_job) + (nterms + up.size()) * sizeof(ntc_gf256_gather_term));
+    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_desc_);
+    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_desc_ + njobs * sizeof(ntc_gf256_gather_job));
+    size_t ji = 0, ti = 0;
+    // copy jobs: staged payload -> its arena slot (coefficient 1)
     size_t pos = 0;
+    uint32_t mx = 16;
     for (Node* c : up) {
-      std::memcpy(h_up_ + pos, c->host.data(), c->size);
+      std::memcpy(h_up_ + pos, c->data(), c->size);
       std::memset(h_up_ + pos + c->size, 0, pad16(c->size) - c->size);
+      c->stage = h_up_ + pos;
       c->chunk = ch;
       c->off = static_cast<uint32_t>(base + pos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
+      jobs[ji] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + c->off), 0,
+                                      static_cast<uint32_t>(ti), 1, c->size, 0};
+      terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(c->stage), c->size, 1};
+      ++ji;
+      mx = std::max<uint32_t>(mx, c->size);
       pos += pad16(c->size);
     }
-    // jobs (by level) and their terms
-    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_desc_);
-    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_desc_ + todo.size() * sizeof(ntc_gf256_gather_job));
-    size_t ti = 0, opos = base + up_bytes;
-    for (size_t j = 0; j < todo.size(); ++j) {
-      Node* n = todo[j];
+    // the jobs (by level) and their terms; a term reads this flush's staged copy when there is one
+    size_t opos = base + up_bytes;
+    for (Node* n : todo) {
       n->chunk = ch;
       n->off = static_cast<uint32_t>(opos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
       opos += pad16(n->size);
-      jobs[j].out = reinterpret_cast<uint64_t>(ch->d + n->off);
-      jobs[j].term0 = static_cast<uint32_t>(ti);
-      jobs[j].nterms = static_cast<uint32_t>(n->expr.size());
-      jobs[j].len = n->size;
-      jobs[j].pad = 0;
+      const uint64_t out2 = n->rpos != kNoPos ? reinterpret_cast<uint64_t>(h_down_ + n->rpos) : 0;
+      jobs[ji++] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + n->off), out2,
+                                        static_cast<uint32_t>(ti), static_cast<uint32_t>(n->expr.size()),
+                                        n->size, 0};
       for (const Term& t : n->expr) {
-        terms[ti].src = reinterpret_cast<uint64_t>(t.node->chunk->d + t.node->off);
-        terms[ti].len = std::min<uint32_t>(t.len, n->size);
-        terms[ti].coef = t.c;
-        ++ti;
+        const Node* c = t.node.get();
+        const uint8_t* src = c->stage ? c->stage : c->chunk->d + c->off;
+        terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(src),
+                                            std::min<uint32_t>(t.len, n->size), t.c};
       }
     }
 #ifndef NTC_CAPI_HOST_STUB
-    if (up_bytes) check(hipMemcpyAsync(ch->d + base, h_up_, up_bytes, hipMemcpyHostToDevice, stream_), "H2D payloads");
-    const size_t desc = todo.size() * sizeof(ntc_gf256_gather_job) + ti * sizeof(ntc_gf256_gather_term);
-    if (desc) check(hipMemcpyAsync(d_desc_, h_desc_, desc, hipMemcpyHostToDevice, stream_), "H2D jobs");
+    const size_t desc = njobs * sizeof(ntc_gf256_gather_job) + ti * sizeof(ntc_gf256_gather_term);
+    check(hipMemcpyAsync(d_desc_, h_desc_, desc, hipMemcpyHostToDevice, stream_), "H2D jobs");
     const auto* djobs = reinterpret_cast<const ntc_gf256_gather_job*>(d_desc_);
-    const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(d_desc_ + todo.size() * sizeof(ntc_gf256_gather_job));
-    for (size_t a = 0; a < todo.size();) {
+    const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(d_desc_ + njobs * sizeof(ntc_gf256_gather_job));
+    // launches: the copy jobs with the first level, then one per further level
+    size_t a = 0;
+    while (a < todo.size()) {
       size_t b = a;
-      uint32_t mx = 1;
-      while (b < todo.size() && todo[b]->level == todo[a]->level) mx = std::max<uint32_t>(mx, todo[b++]->size);
-      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(b - a), djobs + a, dterms, mx, stream_))
+      uint32_t m = a == 0 ? mx : 1u;
+      while (b < todo.size() && todo[b]->level == todo[a]->level) m = std::max<uint32_t>(m, todo[b++]->size);
+      const size_t j0 = a == 0 ? 0 : up.size() + a;
+      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(up.size() + b - j0), djobs + j0, dterms, m, stream_))
         throw device_error(ntc_gf256_last_error());
       a = b;
     }
-    if (out_bytes)
-      check(hipMemcpyAsync(h_down_, ch->d + base + up_bytes, out_bytes, hipMemcpyDeviceToHost, stream_), "D2H results");
-    std::vector<std::pair<Node*, size_t>> late_pos;
-    size_t lp = out_bytes;
+    size_t lp = root_bytes;
     for (Node* r : late) {
+      r->rpos = static_cast<uint32_t>(lp);
       check(hipMemcpyAsync(h_down_ + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
-      late_pos.push_back({r, lp});
       lp += pad16(r->size);
     }
     check(hipStreamSynchronize(stream_), "sync");
 #else
-    std::memset(h_down_, 0, out_bytes);
-    std::vector<std::pair<Node*, size_t>> late_pos;
+    std::memset(h_down_, 0, root_bytes + late_bytes);
+    size_t lp = root_bytes;
+    for (Node* r : late) {
+      r->rpos = static_cast<uint32_t>(lp);
+      lp += pad16(r->size);
+    }
 #endif
     ++launches_;
+    for (Node* c : up) c->stage = nullptr;
     for (Node* n : todo) {
       n->done = true;
       n->expr.clear();
     }
-    // the roots' values (results of this flush from the region copy, earlier ones from theirs)
     for (Node* r : roots) {
-      if (!r->derived || r->fetched) continue;
-      size_t at = 0;
-      bool have = false;
-      if (r->chunk == ch && r->off >= base + up_bytes && r->off < base + up_bytes + out_bytes) {
-        at = r->off - base - up_bytes;
-        have = true;
-      } else {
-        for (const auto& lpp : late_pos)
-          if (lpp.first == r) { at = lpp.second; have = true; }
-      }
-      if (!have) continue;
-      r->host.assign(h_down_ + at, h_down_ + at + r->size);
+      if (!r->derived || r->fetched || r->rpos == kNoPos) continue;
+      r->host.assign(h_down_ + r->rpos, h_down_ + r->rpos + r->size);
       r->fetched = true;
+      r->rpos = kNoPos;
     }
   }
 
@@ -630,17 +657,27 @@ struct Reader {
   void need(size_t n) const { if (left < n) throw overflow_error(); }
   std::vector<uint32_t> ids()                   // packetizer.hh:312-352 (sorted, unique)
   {
-    std::set<uint32_t> s;
+    std::vector<uint32_t> v;
     const uint16_t ne = u16();
-    if (ne == 0) return {};
+    if (ne == 0) return v;
     uint32_t acc = u32();
-    s.insert(acc);
+    v.reserve(32);
+    v.push_back(acc);
+    bool sorted = true;                         // the writer's RLE of ascending ids: already a set
     for (uint32_t i = 0; i + 1u < ne; ++i) {
       const uint8_t run = u8();
       const uint16_t d = u16();
-      for (uint32_t j = 0; j < run; ++j) { acc += d; s.insert(acc); }
+      for (uint32_t j = 0; j < run; ++j) {
+        acc += d;
+        sorted = sorted && acc > v.back();
+        v.push_back(acc);
+      }
     }
-    return std::vector<uint32_t>(s.begin(), s.end());
+    if (!sorted) {                              // a hand-made list: the reference's std::set order
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
+    return v;
   }
 };
 
@@ -655,8 +692,13 @@ struct ntc_packet_t {
   static constexpr size_t shift = 9;   // 16 - 7-byte header (packet.hh:30-36)
   ntcx::bytes v;
   explicit ntc_packet_t(size_t n) : v(n + shift, 0) {}
-  uint8_t* data() { return v.data() + shift; }
-  size_t size() const { return v.size() - shift; }
+  // a packet handed to an encoder / decoder is moved from (empty, size 0) until resized
+  uint8_t* data()
+  {
+    static uint8_t none[16];
+    return v.size() >= shift ? v.data() + shift : none;
+  }
+  size_t size() const { return v.size() >= shift ? v.size() - shift : 0; }
 };
 
 namespace ntcx {
@@ -703,7 +745,7 @@ class Encoder {
       out_.u8(2);                                  // packetizer.hh:165-183
       out_.u32(s.id);
       out_.u16(s.sym->size);
-      out_.raw(s.sym->host.data(), s.sym->size);
+      out_.raw(s.sym->data(), s.sym->size);
       out_.end();
       finish(std::move(p));
     } else {
@@ -729,7 +771,7 @@ class Encoder {
       if (batch_) {
         terms.push_back(Term{s.sym, c, sz});       // distinct window sources: no merging
       } else {
-        in_.push_back(s.sym->host.data());
+        in_.push_back(s.sym->data());
         lens_.push_back(sz);
         cs_.push_back(c);
       }
@@ -823,11 +865,7 @@ class Encoder {
     NodeRef sym;                       // immutable once in the window (shared with pending repairs)
   };
   // batch mode: the packet is built into p.pkt (begin) and queued in the batch (finish)
-  void begin(Pending& p, size_t reserve)
-  {
-    out_.buf = batch_ ? &p.pkt : nullptr;
-    if (batch_) p.pkt.reserve(reserve);
-  }
+  void begin(Pending& p, size_t reserve);
   void finish(Pending&& p);
 
   Field f_;
@@ -863,8 +901,9 @@ class Decoder {
   const ntc_packet_handler& packet_handler() const { return out_.h; }
   const ntc_data_handler& data_handler() const { return dh_; }
 
-  // decoder.hh:88-122
-  size_t add_packet(const uint8_t* p, size_t n)
+  // decoder.hh:88-122.  own: the buffer p lies in, when the caller hands it over (the C ABI
+  // moves the packet in, like the reference): a batched decoder keeps the payload in it.
+  size_t add_packet(const uint8_t* p, size_t n, bytes* own = nullptr)
   {
     if (n == 0) throw overflow_error();
     Reader rd{p, n};
@@ -878,7 +917,7 @@ class Decoder {
       std::vector<uint32_t> ids = rd.ids();
       const uint16_t esz = rd.u16();
       const size_t consumed = n - rd.left;
-      if (!ids.empty()) on_repair(id, std::move(ids), esz, sym, symsz);
+      if (!ids.empty()) on_repair(id, std::move(ids), esz, sym, symsz, own);
       return consumed;
     }
     if (ty == 2) {
@@ -888,7 +927,7 @@ class Decoder {
       const uint16_t sz = rd.u16();
       const uint8_t* sym = rd.skip(sz);
       const size_t consumed = n - rd.left;
-      on_source(id, sym, sz);
+      on_source(id, sym, sz, own);
       return consumed;
     }
     throw packet_type_error();
@@ -1021,6 +1060,7 @@ class Decoder {
   {
     if (known.empty()) return;
     if (batch_) {                // one term per source payload, whatever produced it
+      r.red.reserve(r.red.size() + known.size());
       for (const Src* s : known) {
         const uint32_t c = f_.coef(r.id, s->id);
         r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
@@ -1062,20 +1102,21 @@ class Decoder {
   }
 
   // detail/decoder.cc:33-50
-  void on_source(uint32_t id, const uint8_t* sym, uint16_t sz)
+  void on_source(uint32_t id, const uint8_t* sym, uint16_t sz, bytes* own = nullptr)
   {
     if (has_last_ && id < last_id_) return;
     if (sources_.count(id)) return;
     Src s{id, bytes(), sz, nullptr};
-    if (batch_) s.node = base_node(sym, sz);
+    if (batch_) s.node = own ? adopt_node(std::move(*own), sym - own->data(), sz) : base_node(sym, sz);
     else s.sym.assign(sym, sym + sz);
-    if (s.sym.empty()) s.sym.resize(1);
+    if (!batch_ && s.sym.empty()) s.sym.resize(1);
     add_source_recursive(std::move(s));
     attempt_full_decoding();
   }
 
   // detail/decoder.cc:54-152
-  void on_repair(uint32_t id, std::vector<uint32_t>&& ids, uint16_t esz, const uint8_t* sym, uint16_t symsz)
+  void on_repair(uint32_t id, std::vector<uint32_t>&& ids, uint16_t esz, const uint8_t* sym, uint16_t symsz,
+                 bytes* own = nullptr)
   {
     if (has_last_ && ids.back() < last_id_) return;
     if (repairs_.count(id)) return;
@@ -1084,9 +1125,11 @@ class Decoder {
     for (uint32_t sid : ids) if (!sources_.count(sid)) { useless = false; break; }
     if (useless) { ++nb_useless_; return; }
     Rep& r = repairs_.emplace(id, Rep{id, std::move(ids), esz, bytes(), symsz, {}}).first->second;
-    if (batch_) r.red.push_back(Term{base_node(sym, symsz), 1, symsz});
+    if (batch_)
+      r.red.push_back(Term{own ? adopt_node(std::move(*own), sym - own->data(), symsz) : base_node(sym, symsz),
+                           1, symsz});
     else r.sym.assign(sym, sym + symsz);
-    if (r.sym.empty()) r.sym.resize(1);
+    if (!batch_ && r.sym.empty()) r.sym.resize(1);
     std::vector<const Src*> known;
     std::vector<uint32_t> remaining;
     for (auto it = r.ids.rbegin(); it != r.ids.rend(); ++it) {
@@ -1345,6 +1388,15 @@ class Batch {
              q_.end());
   }
   void push(Pending&& p) { q_.push_back(std::move(p)); }
+  // a packet buffer of an already flushed event (empty, capacity kept), or a new one
+  bytes take_buffer()
+  {
+    if (pool_.empty()) return bytes();
+    bytes b = std::move(pool_.back());
+    pool_.pop_back();
+    b.clear();
+    return b;
+  }
   size_t pending() const { return q_.size(); }
   void flush();
 
@@ -1352,6 +1404,8 @@ class Batch {
   std::vector<Encoder*> encs_;
   std::vector<Decoder*> decs_;
   std::vector<Pending> q_;
+  std::vector<Pending> spare_;   // the last flushed queue's storage, reused by the next one
+  std::vector<bytes> pool_;      // flushed packets' buffers (no malloc / free per packet)
 };
 
 Encoder::~Encoder()
@@ -1368,6 +1422,15 @@ void Encoder::set_batch(Batch* b)
   }
   batch_ = b;
   if (b) b->attach(this);
+}
+
+void Encoder::begin(Pending& p, size_t reserve)
+{
+  out_.buf = batch_ ? &p.pkt : nullptr;
+  if (batch_) {
+    p.pkt = batch_->take_buffer();
+    p.pkt.reserve(reserve);
+  }
 }
 
 void Encoder::finish(Pending&& p)
@@ -1400,7 +1463,7 @@ void Decoder::set_batch(Batch* b)
     }
     if (!roots.empty()) Device::get().evaluate(roots);
     auto host_bytes = [](const Node& n, uint16_t size) {
-      bytes v(n.host.begin(), n.host.begin() + std::min<size_t>(n.host.size(), size));
+      bytes v(n.data(), n.data() + std::min<size_t>(n.host.size() - n.hoff, size));
       v.resize(std::max<size_t>(size, 1), 0);
       return v;
     };
@@ -1447,23 +1510,28 @@ void Batch::flush()
   if (!roots.empty()) Device::get().evaluate(roots);
   std::vector<Pending> q;
   q.swap(q_);
+  if (q_.capacity() < spare_.capacity()) q_.swap(spare_);   // keep the queue's storage warm
   for (Pending& p : q) {
     if (p.kind == Pending::DEC_DATA) {
       const ntc_data_handler& h = p.dec->data_handler();
       static const uint8_t zero[16] = {0};
-      const uint8_t* d = p.size ? p.node->host.data() : zero;
+      const uint8_t* d = p.size ? p.node->data() : zero;
       h.read_data(h.context, reinterpret_cast<const char*>(d), p.size);
       continue;
     }
     if (p.node) {                        // encoder repair: both copies of the symbol
-      std::memcpy(p.pkt.data() + p.off1, p.node->host.data(), p.size);
-      std::memcpy(p.pkt.data() + p.off2, p.node->host.data(), p.size);
+      std::memcpy(p.pkt.data() + p.off1, p.node->data(), p.size);
+      std::memcpy(p.pkt.data() + p.off2, p.node->data(), p.size);
     }
     const ntc_packet_handler& h = p.kind == Pending::ENC_PACKET ? p.enc->handler()
                                                                 : p.dec->packet_handler();
     h.prepare_packet(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.pkt.size());
     h.send_packet(h.context);
   }
+  for (Pending& p : q)
+    if (p.pkt.capacity() && pool_.size() < 16384) pool_.push_back(std::move(p.pkt));
+  q.clear();
+  spare_.swap(q);
 }
 
 // c/detail/check_error.hh: exceptions -> ntc_error (message in thread-local storage).
@@ -1565,8 +1633,8 @@ void ntc_encoder_add_data(ntc_encoder_t* enc, ntc_data_t* data, ntc_error* error
 size_t ntc_encoder_add_packet(ntc_encoder_t* enc, ntc_packet_t* packet, ntc_error* error) noexcept
 {
   return ntcx::guarded([&] {
-    ntcx::bytes v = std::move(packet->v);
-    packet->v = ntcx::bytes(ntc_packet_t::shift, 0);
+    ntcx::bytes v = std::move(packet->v);          // the packet is left empty (moved from)
+    if (v.size() < ntc_packet_t::shift) v.resize(ntc_packet_t::shift, 0);
     const size_t n = v.size() - ntc_packet_t::shift;
     return enc->e.add_packet(v.data() + ntc_packet_t::shift, n);
   }, error);
@@ -1595,10 +1663,10 @@ void ntc_delete_decoder(ntc_decoder_t* dec) noexcept { delete dec; }
 size_t ntc_decoder_add_packet(ntc_decoder_t* dec, ntc_packet_t* packet, ntc_error* error) noexcept
 {
   return ntcx::guarded([&] {
-    ntcx::bytes v = std::move(packet->v);
-    packet->v = ntcx::bytes(ntc_packet_t::shift, 0);
+    ntcx::bytes v = std::move(packet->v);          // the packet is left empty (moved from)
+    if (v.size() < ntc_packet_t::shift) v.resize(ntc_packet_t::shift, 0);
     const size_t n = v.size() - ntc_packet_t::shift;
-    return dec->d.add_packet(v.data() + ntc_packet_t::shift, n);
+    return dec->d.add_packet(v.data() + ntc_packet_t::shift, n, &v);
   }, error);
 }
 void ntc_decoder_generate_ack(ntc_decoder_t* dec, ntc_error* error) noexcept

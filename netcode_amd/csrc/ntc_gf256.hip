@@ -1993,10 +1993,12 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 __global__ __launch_bounds__(64) void gather_combine(const ntc_gf256_gather_job* __restrict__ jobs,
                                                      const ntc_gf256_gather_term* __restrict__ terms)
 {
-  static_assert(sizeof(ntc_gf256_gather_job) == 24 && sizeof(ntc_gf256_gather_term) == 16, "layout");
-  const u32x4 j4 = const_load<u32x4>(jobs + blockIdx.x);           // out (2 dwords), term0, nterms
-  const uint32_t jlen = const_load<uint32_t>(reinterpret_cast<const uint8_t*>(jobs + blockIdx.x) + 16);
+  static_assert(sizeof(ntc_gf256_gather_job) == 32 && sizeof(ntc_gf256_gather_term) == 16, "layout");
+  const u32x8 j8 = const_load<u32x8>(jobs + blockIdx.x);   // out (2 dwords), out2 (2), term0, nterms, len
+  const u32x4 j4 = {j8[0], j8[1], j8[4], j8[5]};
+  const uint32_t jlen = j8[6];
   uint8_t* out = reinterpret_cast<uint8_t*>((static_cast<uint64_t>(j4[1]) << 32) | j4[0]);
+  uint8_t* out2 = reinterpret_cast<uint8_t*>((static_cast<uint64_t>(j8[3]) << 32) | j8[2]);
   const uint32_t col = blockIdx.y * 1024u + threadIdx.x * 16u;
   if (col >= ((jlen + 15u) & ~15u)) return;
   uint32_t acc[4] = {0, 0, 0, 0};
@@ -2021,6 +2023,7 @@ __global__ __launch_bounds__(64) void gather_combine(const ntc_gf256_gather_job*
     for (int d = 0; d < 4; ++d) acc[d] ^= mul4(tf, x[d]);
   }
   *reinterpret_cast<uint4*>(out + col) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+  if (out2) *reinterpret_cast<uint4*>(out2 + col) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
 }
 
 __global__ __launch_bounds__(256) void region_mul(const uint8_t* __restrict__ src,

@@ -1,6 +1,6 @@
 """Flat and inclusive profile from tools/sampler.c's sample file.
 
-usage: python tools/sampler_report.py [/tmp/ntc_samples.txt] [top N]
+usage: python tools/sampler_report.py [/tmp/ntc_samples.txt] [top N] [obj,obj (resolve with addr2line)]
 Symbols come from `nm -C --defined-only` of each mapped object (text symbols, nearest below).
 """
 import bisect
@@ -28,6 +28,8 @@ _syms = {}
 def symbols(obj):
     if obj not in _syms:
         out = subprocess.run(["nm", "-C", "--defined-only", obj], capture_output=True, text=True).stdout
+        if not out.strip():                      # stripped: the dynamic symbol table
+            out = subprocess.run(["nm", "-C", "-D", "--defined-only", obj], capture_output=True, text=True).stdout
         tab = []
         for ln in out.splitlines():
             p = ln.split(" ", 2)
@@ -38,14 +40,47 @@ def symbols(obj):
     return _syms[obj]
 
 
-def resolve(maps, pc):
+_a2l = {}
+_segs = {}
+
+
+def to_vaddr(obj, a):
+    """File offset -> link-time address (lld places text at offset + 0x1000 and the like)."""
+    if obj not in _segs:
+        out = subprocess.run(["readelf", "-lW", obj], capture_output=True, text=True).stdout
+        segs = []
+        for ln in out.splitlines():
+            f = ln.split()
+            if f and f[0] == "LOAD":
+                segs.append((int(f[1], 16), int(f[2], 16), int(f[4], 16)))
+        _segs[obj] = segs
+    for off, va, sz in _segs[obj]:
+        if off <= a < off + sz:
+            return a - off + va
+    return a
+
+
+def addr2line(obj, addrs):
+    """Function names of file offsets in obj via addr2line (objects built with -g), cached."""
+    todo = sorted({a for a in addrs if (obj, a) not in _a2l})
+    if todo:
+        out = subprocess.run(["addr2line", "-f", "-C", "-e", obj] + [hex(a) for a in todo],
+                             capture_output=True, text=True).stdout.splitlines()
+        for i, a in enumerate(todo):
+            _a2l[(obj, a)] = out[2 * i] if 2 * i < len(out) else "?"
+
+
+def resolve(maps, pc, dbg=()):
     for lo, hi, off, obj in maps:
         if lo <= pc < hi:
-            # PIE / shared objects: file offset of the pc; nm addresses ~ file offsets for text
-            a = pc - lo + off
-            addrs, names = symbols(obj)
-            i = bisect.bisect_right(addrs, a) - 1
-            name = names[i] if i >= 0 else "?"
+            a = to_vaddr(obj, pc - lo + off)
+            if obj in dbg:
+                addr2line(obj, [a])
+                name = _a2l[(obj, a)]
+            else:
+                addrs, names = symbols(obj)
+                i = bisect.bisect_right(addrs, a) - 1
+                name = names[i] if i >= 0 else "?"
             return f"{obj.rsplit('/', 1)[-1]}:{name[:110]}"
     return "?"
 
@@ -54,9 +89,13 @@ def main():
     path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/ntc_samples.txt"
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     maps, samples = load(path)
+    dbg = set(sys.argv[3].split(",")) if len(sys.argv) > 3 else set()
+    for lo, hi, off, obj in maps:                  # batch the addr2line calls
+        if obj in dbg:
+            addr2line(obj, [to_vaddr(obj, pc - lo + off) for s in samples for pc in s if lo <= pc < hi])
     self_c, incl_c = collections.Counter(), collections.Counter()
     for s in samples:
-        names = [resolve(maps, pc) for pc in s if pc]
+        names = [resolve(maps, pc, dbg) for pc in s if pc]
         if not names:
             continue
         self_c[names[0]] += 1

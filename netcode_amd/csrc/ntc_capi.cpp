@@ -97,7 +97,6 @@ struct Node {
   uint32_t off = 0;
   int level = 0;               // flush bookkeeping: evaluation level, visit stamp
   uint64_t mark = 0;
-  const uint8_t* stage = nullptr;   // during a flush: the pinned staged copy this flush uploads
   uint32_t rpos = ~0u;         // during a flush: offset of the fetched value in the result staging
   ~Node()
   {
@@ -344,11 +343,10 @@ class Device {
     return cur_;
   }
 
-  // One flush of GF(2^8) jobs.  The payloads the jobs read that are not on the device yet are
-  // staged in pinned host memory: the jobs of this flush read them from there, and copy jobs in
-  // the same launch store them into the arena for later flushes.  A root's result is written by
-  // its job both into the arena and straight into pinned host memory (the job's second output),
-  // so a flush is one descriptor copy, one launch per dependency level and one synchronisation.
+  // One flush of GF(2^8) jobs: the payloads the jobs read that are not on the device yet and the
+  // job / term descriptors go up in ONE copy into the flush's arena region; a root's result is
+  // written by its job both into the arena and straight into pinned host memory (the job's second
+  // output), so a flush is one copy, one launch per dependency level and one synchronisation.
   void evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep)
   {
     const uint64_t up_mark = ep + (1ull << 63);
@@ -379,62 +377,49 @@ class Device {
       }
     }
     if (todo.empty() && late.empty()) return;
+    // flush region of the arena: [uploaded payloads | descriptors | job outputs]
+    const size_t desc = pad16(todo.size() * sizeof(ntc_gf256_gather_job) + nterms * sizeof(ntc_gf256_gather_term));
+    const size_t region = up_bytes + (todo.empty() ? 0 : desc) + out_bytes;
     size_t base = 0;
-    DevChunk* ch = (up_bytes + out_bytes) ? arena_alloc(up_bytes + out_bytes, &base) : nullptr;
-    const size_t njobs = up.size() + todo.size();
-    grow_stage(up_bytes, root_bytes + late_bytes,
-               njobs * sizeof(ntc_gf256_gather_job) + (nterms + up.size()) * sizeof(ntc_gf256_gather_term));
-    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_desc_);
-    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_desc_ + njobs * sizeof(ntc_gf256_gather_job));
-    size_t ji = 0, ti = 0;
-    // copy jobs: staged payload -> its arena slot (coefficient 1)
+    DevChunk* ch = region ? arena_alloc(region, &base) : nullptr;
+    grow_stage(up_bytes + desc, root_bytes + late_bytes);
     size_t pos = 0;
-    uint32_t mx = 16;
     for (Node* c : up) {
       std::memcpy(h_up_ + pos, c->data(), c->size);
       std::memset(h_up_ + pos + c->size, 0, pad16(c->size) - c->size);
-      c->stage = h_up_ + pos;
       c->chunk = ch;
       c->off = static_cast<uint32_t>(base + pos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
-      jobs[ji] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + c->off), 0,
-                                      static_cast<uint32_t>(ti), 1, c->size, 0};
-      terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(c->stage), c->size, 1};
-      ++ji;
-      mx = std::max<uint32_t>(mx, c->size);
       pos += pad16(c->size);
     }
-    // the jobs (by level) and their terms; a term reads this flush's staged copy when there is one
-    size_t opos = base + up_bytes;
-    for (Node* n : todo) {
+    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_up_ + up_bytes);
+    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_up_ + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
+    size_t ti = 0, opos = base + up_bytes + desc;
+    for (size_t j = 0; j < todo.size(); ++j) {
+      Node* n = todo[j];
       n->chunk = ch;
       n->off = static_cast<uint32_t>(opos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
       opos += pad16(n->size);
       const uint64_t out2 = n->rpos != kNoPos ? reinterpret_cast<uint64_t>(h_down_ + n->rpos) : 0;
-      jobs[ji++] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + n->off), out2,
-                                        static_cast<uint32_t>(ti), static_cast<uint32_t>(n->expr.size()),
-                                        n->size, 0};
-      for (const Term& t : n->expr) {
-        const Node* c = t.node.get();
-        const uint8_t* src = c->stage ? c->stage : c->chunk->d + c->off;
-        terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(src),
+      jobs[j] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + n->off), out2,
+                                     static_cast<uint32_t>(ti), static_cast<uint32_t>(n->expr.size()),
+                                     n->size, 0};
+      for (const Term& t : n->expr)
+        terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(t.node->chunk->d + t.node->off),
                                             std::min<uint32_t>(t.len, n->size), t.c};
-      }
     }
 #ifndef NTC_CAPI_HOST_STUB
-    const size_t desc = njobs * sizeof(ntc_gf256_gather_job) + ti * sizeof(ntc_gf256_gather_term);
-    check(hipMemcpyAsync(d_desc_, h_desc_, desc, hipMemcpyHostToDevice, stream_), "H2D jobs");
-    const auto* djobs = reinterpret_cast<const ntc_gf256_gather_job*>(d_desc_);
-    const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(d_desc_ + njobs * sizeof(ntc_gf256_gather_job));
-    // launches: the copy jobs with the first level, then one per further level
-    size_t a = 0;
-    while (a < todo.size()) {
+    if (!todo.empty())
+      check(hipMemcpyAsync(ch->d + base, h_up_, up_bytes + desc, hipMemcpyHostToDevice, stream_), "H2D payloads + jobs");
+    const auto* djobs = reinterpret_cast<const ntc_gf256_gather_job*>(todo.empty() ? nullptr : ch->d + base + up_bytes);
+    const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(
+        todo.empty() ? nullptr : ch->d + base + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
+    for (size_t a = 0; a < todo.size();) {
       size_t b = a;
-      uint32_t m = a == 0 ? mx : 1u;
+      uint32_t m = 1;
       while (b < todo.size() && todo[b]->level == todo[a]->level) m = std::max<uint32_t>(m, todo[b++]->size);
-      const size_t j0 = a == 0 ? 0 : up.size() + a;
-      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(up.size() + b - j0), djobs + j0, dterms, m, stream_))
+      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(b - a), djobs + a, dterms, m, stream_))
         throw device_error(ntc_gf256_last_error());
       a = b;
     }
@@ -454,7 +439,6 @@ class Device {
     }
 #endif
     ++launches_;
-    for (Node* c : up) c->stage = nullptr;
     for (Node* n : todo) {
       n->done = true;
       n->expr.clear();
@@ -467,7 +451,7 @@ class Device {
     }
   }
 
-  void grow_stage(size_t up, size_t down, size_t desc)
+  void grow_stage(size_t up, size_t down)
   {
     auto up_h = [](uint8_t** h, size_t* cap, size_t need) {
       if (need <= *cap) return;
@@ -484,19 +468,6 @@ class Device {
     };
     up_h(&h_up_, &cap_up_, up + 16);
     up_h(&h_down_, &cap_down_, down + 16);
-    up_h(&h_desc_, &cap_desc_, desc + 64);
-    if (desc + 64 > cap_ddesc_) {
-      const size_t n = std::max(desc + 64, cap_ddesc_ * 2);
-#ifdef NTC_CAPI_HOST_STUB
-      std::free(d_desc_);
-      d_desc_ = static_cast<uint8_t*>(std::malloc(n));
-#else
-      if (d_desc_) (void)hipFree(d_desc_);
-      d_desc_ = nullptr;
-      check(hipMalloc(reinterpret_cast<void**>(&d_desc_), n), "hipMalloc jobs");
-#endif
-      cap_ddesc_ = n;
-    }
   }
 
   // combine_generations without taking mu_ (the caller holds it)
@@ -520,7 +491,43 @@ class Device {
       err_ = "hipStreamCreate failed";
       ntc_gf256_engine_destroy(eng_);
       eng_ = nullptr;
+      return;
     }
+    try {
+      warm_up();
+    } catch (const std::exception& e) {
+      err_ = e.what();
+      ntc_gf256_engine_destroy(eng_);
+      eng_ = nullptr;
+    }
+  }
+
+  // Once per process, when the first encoder / decoder is made: pinned staging and a first
+  // arena chunk, and one flush-shaped round trip (copy engine, gather kernel) so that no
+  // first-use initialisation (tens of ms on a fresh process) lands in a packet's call.
+  void warm_up()
+  {
+    grow_stage(size_t(4) << 20, size_t(4) << 20);
+    size_t off = 0;
+    DevChunk* ch = arena_alloc(96, &off);        // [source 16 | job 32 | term 16 | output 16]
+    auto* job = reinterpret_cast<ntc_gf256_gather_job*>(h_up_ + 16);
+    auto* term = reinterpret_cast<ntc_gf256_gather_term*>(h_up_ + 16 + sizeof(ntc_gf256_gather_job));
+    std::memset(h_up_, 0, 16);
+    *term = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(ch->d + off), 16, 1};
+    *job = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + off + 64), reinterpret_cast<uint64_t>(h_down_),
+                                0, 1, 16, 0};
+    check(hipMemcpyAsync(ch->d + off, h_up_, 64, hipMemcpyHostToDevice, stream_), "warm-up H2D");
+    // a flush-sized copy too: large copies take another path (copy engine) with its own first use
+    size_t boff = 0;
+    DevChunk* bch = arena_alloc(size_t(512) << 10, &boff);
+    check(hipMemcpyAsync(bch->d + boff, h_up_, size_t(512) << 10, hipMemcpyHostToDevice, stream_), "warm-up H2D");
+    if (ntc_gf256_gather_combine(eng_, 1, reinterpret_cast<const ntc_gf256_gather_job*>(ch->d + off + 16),
+                                 reinterpret_cast<const ntc_gf256_gather_term*>(ch->d + off + 16 + sizeof(ntc_gf256_gather_job)),
+                                 16, stream_))
+      throw device_error(ntc_gf256_last_error());
+    check(hipMemcpyAsync(h_down_ + 16, ch->d + off + 64, 16, hipMemcpyDeviceToHost, stream_), "warm-up D2H");
+    check(hipStreamSynchronize(stream_), "warm-up sync");
+    cur_->used = 0;                              // the chunk holds nothing live
   }
   ~Device()
   {
@@ -567,8 +574,8 @@ class Device {
   std::vector<DevChunk*> chunks_;
   DevChunk* cur_ = nullptr;
   uint64_t epoch_ = 0;
-  uint8_t *h_up_ = nullptr, *h_down_ = nullptr, *h_desc_ = nullptr, *d_desc_ = nullptr;
-  size_t cap_up_ = 0, cap_down_ = 0, cap_desc_ = 0, cap_ddesc_ = 0;
+  uint8_t *h_up_ = nullptr, *h_down_ = nullptr;   // pinned: flush uploads / results
+  size_t cap_up_ = 0, cap_down_ = 0;
 };
 
 template <typename Fill, typename Sink>

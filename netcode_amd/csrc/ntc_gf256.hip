@@ -805,7 +805,21 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
   const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
   const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
   uint16_t* pw = part[wv];
-  uint32_t lmax = 0;
+  // source lengths: max (the repair length) and whether they are all equal -- then a repair's
+  // encoded size is multiply_size(L, XOR of its coefficients) (the product distributes over XOR),
+  // one product per repair instead of one per source
+  uint32_t lmax = 0, lmin = 0xFFFFu;
+  for (uint32_t i = lane; i < a.k; i += 64u) {
+    const uint32_t l = len[i];
+    lmax = max(lmax, l);
+    lmin = min(lmin, l);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lmax = max(lmax, static_cast<uint32_t>(__shfl_xor(lmax, o)));
+    lmin = min(lmin, static_cast<uint32_t>(__shfl_xor(lmin, o)));
+  }
+  const bool same_len = uniform(lmin) == uniform(lmax);
   // pairing: a first-of-pair generation also walks its partner's coefficients and compares them
   // (only when the partner's id bases are congruent mod 255, the necessary condition)
   const bool first = a.pair && (g / kPairGap) % 2u == 0u;
@@ -827,16 +841,18 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
     CoefWalk cp[4] = {CoefWalk(pridb + 4u * w + 1u, psidb + q + 1u, nq), CoefWalk(pridb + 4u * w + 2u, psidb + q + 1u, nq),
                       CoefWalk(pridb + 4u * w + 3u, psidb + q + 1u, nq), CoefWalk(pridb + 4u * w + 4u, psidb + q + 1u, nq)};
     uint32_t esz[4] = {0, 0, 0, 0};
+    uint32_t csum = 0;                            // same_len: XOR of the coefficient words
     // four sources per pass, their lengths loaded together (one memory round trip per 4)
     for (uint32_t ib = q; ib < a.k; ib += 4u * nq) {
-      uint32_t lq[4];
+      uint32_t lq[4] = {0, 0, 0, 0};
+      if (!same_len) {
 #pragma unroll
-      for (uint32_t e = 0; e < 4; ++e) lq[e] = ib + e * nq < a.k ? len[ib + e * nq] : 0u;
+        for (uint32_t e = 0; e < 4; ++e) lq[e] = ib + e * nq < a.k ? len[ib + e * nq] : 0u;
+      }
 #pragma unroll
       for (uint32_t e = 0; e < 4; ++e) {
         const uint32_t i = ib + e * nq;
         if (i >= a.k) break;
-        lmax = max(lmax, lq[e]);
         uint32_t word = 0, pword = 0;
 #pragma unroll
         for (uint32_t b = 0; b < 4; ++b) {
@@ -845,15 +861,20 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
             word |= c << (8 * b);
             // both length bytes times c in one v_perm lookup (galois_field.hh:108-115 codes a
             // u16 as a 2-byte region; a zero length stays zero)
-            esz[b] ^= mul4(tabs[c], lq[e]);
+            if (!same_len) esz[b] ^= mul4(tabs[c], lq[e]);
             if (cmp) pword |= cp[b].coef() << (8 * b);
           }
           cw[b].next();
           if (cmp) cp[b].next();
         }
+        csum ^= word;
         diff |= word ^ pword;
         *reinterpret_cast<uint32_t*>(coef + static_cast<size_t>(i) * a.rp) = word;
       }
+    }
+    if (same_len) {
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) esz[b] = mul4(tabs[(csum >> (8 * b)) & 0xFFu], lmax);
     }
 #pragma unroll
     for (uint32_t b = 0; b < 4; ++b) pw[q * a.rp + 4u * w + b] = static_cast<uint16_t>(esz[b]);
@@ -874,11 +895,7 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
     for (uint32_t s2 = 0; s2 < nq; ++s2) e ^= pw[s2 * a.rp + j];
     a.rep_size[static_cast<size_t>(g) * a.r + j] = e;
   }
-  if (a.rep_len) {                                // repair length = max source length
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) lmax = max(lmax, static_cast<uint32_t>(__shfl_xor(lmax, o)));
-    if (lane == 0) a.rep_len[g] = static_cast<uint16_t>(lmax);
-  }
+  if (a.rep_len && lane == 0) a.rep_len[g] = static_cast<uint16_t>(lmax);   // max source length
 }
 
 // One 64-thread block (one wave) per generation.  Reproduces what ntc::detail::decoder does when

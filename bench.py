@@ -79,6 +79,7 @@ def parse():
     pp.add_argument("--rate", type=int, default=4)
     pp.add_argument("--loss", type=float, default=0.1)
     pp.add_argument("--c-items", type=int, default=128, help="items per flow of the C-level legs")
+    pp.add_argument("--pp-reps", type=int, default=3, help="interleaved runs of each C-level leg (best kept)")
     return p.parse_args()
 
 
@@ -468,29 +469,42 @@ def per_packet_main(a):
     import subprocess
     drv = os.path.join(ROOT, "tests", "_build", "pp_driver")
     cargs = [str(x) for x in (a.flows, a.c_items, a.size, a.window, a.rate, int(round(a.loss * 100)), 7)]
-    c_gpu = {}
-    for mode in ("immediate", "batched"):
+    # each C-level leg runs `reps` times, interleaved (host load on the box drifts), best kept
+    def run_gpu(mode):
         out = subprocess.run([drv, mode] + cargs, capture_output=True, text=True, timeout=600)
         if out.returncode != 0:
             raise RuntimeError(f"pp_driver {mode} failed: {out.stderr[-400:]}")
-        c_gpu[mode] = json.loads(out.stdout.strip().splitlines()[-1])
-    secs = (C.c_double * 2)()
-    cnt = (C.c_uint64 * 4)()
-    hs = (C.c_uint64 * 2)()
-    L.or_set_simd(1)
-    try:
-        L.or_pp_bench(a.flows, a.c_items, a.size, a.window, a.rate, int(round(a.loss * 100)),
-                      C.c_uint64(7), secs, cnt, hs)
-    finally:
-        L.or_set_simd(0)
-    c_cpu = {"encode_s": secs[0], "decode_s": secs[1], "packets": cnt[0], "received": cnt[1],
-             "deliveries": cnt[2], "repairs": cnt[3], "packets_hash": f"{hs[0]:016x}",
-             "deliveries_hash": f"{hs[1]:016x}"}
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    def run_cpu():
+        secs = (C.c_double * 2)()
+        cnt = (C.c_uint64 * 4)()
+        hs = (C.c_uint64 * 2)()
+        L.or_set_simd(1)
+        try:
+            L.or_pp_bench(a.flows, a.c_items, a.size, a.window, a.rate, int(round(a.loss * 100)),
+                          C.c_uint64(7), secs, cnt, hs)
+        finally:
+            L.or_set_simd(0)
+        return {"encode_s": secs[0], "decode_s": secs[1], "packets": cnt[0], "received": cnt[1],
+                "deliveries": cnt[2], "repairs": cnt[3], "packets_hash": f"{hs[0]:016x}",
+                "deliveries_hash": f"{hs[1]:016x}"}
+
+    runs = {"immediate": [], "batched": [], "cpu": []}
+    for _ in range(a.pp_reps):
+        runs["batched"].append(run_gpu("batched"))
+        runs["cpu"].append(run_cpu())
+        runs["immediate"].append(run_gpu("immediate"))
+    best = lambda rs: min(rs, key=lambda r: r["encode_s"] + r["decode_s"])
+    c_gpu = {m: best(runs[m]) for m in ("immediate", "batched")}
+    c_cpu = best(runs["cpu"])
+    for m, rs in runs.items():
+        (c_cpu if m == "cpu" else c_gpu[m])["all_runs_s"] = [round(r["encode_s"] + r["decode_s"], 5) for r in rs]
     cpps = lambda r: round((r["packets"] + r["received"]) / (r["encode_s"] + r["decode_s"]), 1)
     for r in list(c_gpu.values()) + [c_cpu]:
         r["packets_per_s"] = cpps(r)
     c_ok = all(r["packets_hash"] == c_cpu["packets_hash"] and
-               r["deliveries_hash"] == c_cpu["deliveries_hash"] for r in c_gpu.values())
+               r["deliveries_hash"] == c_cpu["deliveries_hash"] for rs in runs.values() for r in rs)
     model, _, _ = cpu_info()
     line = {"metric": "per-packet drop-in encode+decode packets/s (C ABI, one object per flow)",
             "value": c_gpu["batched"]["packets_per_s"], "unit": "packets/s", "n_gpus": 1,
@@ -501,7 +515,7 @@ def per_packet_main(a):
                        ("flows", "c_items", "size", "window", "rate", "loss")}},
             "value_note": "C-level driver (tools/pp_driver.c), GPU region ops batched across flows "
                           "(ntc_batch_t); packets encoded + packets received, over encode + "
-                          "decode time",
+                          "decode time; best of the interleaved runs of each leg (all_runs_s)",
             "c_level": {"gpu_batched": c_gpu["batched"], "gpu_immediate": c_gpu["immediate"],
                         "cpu_oracle": c_cpu},
             "cpu_baseline": {"value": c_cpu["packets_per_s"], "unit": "packets/s", "cores": 1,

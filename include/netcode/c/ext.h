@@ -23,14 +23,17 @@ size_t ntc_encoder_counter(const ntc_encoder_t* enc, int which) NTC_C_NOEXCEPT N
 size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT NTC_C_NONNULL;
 
 /* Online batching adaptor.  Encoders and decoders attached to a batch queue
- * every packet and data delivery they produce instead of calling their handlers.  Their protocol
- * state (windows, rates, counters, missing / pending sets, acks) advances immediately -- the
- * reference's control flow never depends on payload bytes -- while each GF region result is kept
- * as a linear expression over the payloads it came from.  ntc_batch_flush evaluates every pending
- * expression (encoder repairs, decoder deliveries) with one GPU launch per Galois field size, then
- * calls the handlers in production order (a packet as one prepare_packet call followed by
+ * the packets and data deliveries that need a GF result (encoder repairs, decoded sources) -- and
+ * everything an object produces after one of its events is queued -- instead of calling their
+ * handlers; an event of an object with nothing queued that needs no GF result (a source packet, a
+ * received source's delivery, an ack) is emitted at once.  Protocol state (windows, rates,
+ * counters, missing / pending sets, acks) advances immediately -- the reference's control flow
+ * never depends on payload bytes -- while each GF region result is kept as a linear expression
+ * over the payloads it came from.  ntc_batch_flush evaluates every pending expression with one
+ * GPU launch per dependency level (payloads resident on the device), then calls the queued
+ * handlers in production order (a queued packet as one prepare_packet call followed by
  * send_packet).  Each object's callback sequence is byte-for-byte the unbatched one
- * (encoder.hh:255-333, decoder.hh:88-300 semantics); only the time of the callbacks moves to the
+ * (encoder.hh:255-333, decoder.hh:88-300 semantics); only the time of some callbacks moves to the
  * flush.  Attaching an object to another batch or to NULL flushes its current batch first.
  * Deleting an attached object discards its queued events; deleting a batch discards every queued
  * event and detaches its objects. */

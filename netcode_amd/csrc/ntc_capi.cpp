@@ -429,7 +429,7 @@ class Device {
       check(hipMemcpyAsync(h_down_ + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
       lp += pad16(r->size);
     }
-    check(hipStreamSynchronize(stream_), "sync");
+    wait_stream();
 #else
     std::memset(h_down_, 0, root_bytes + late_bytes);
     size_t lp = root_bytes;
@@ -493,6 +493,12 @@ class Device {
       eng_ = nullptr;
       return;
     }
+    if (hipEventCreateWithFlags(&done_, hipEventDisableTiming) != hipSuccess) {
+      err_ = "hipEventCreate failed";
+      ntc_gf256_engine_destroy(eng_);
+      eng_ = nullptr;
+      return;
+    }
     try {
       warm_up();
     } catch (const std::exception& e) {
@@ -500,6 +506,18 @@ class Device {
       ntc_gf256_engine_destroy(eng_);
       eng_ = nullptr;
     }
+  }
+
+  // Wait for the flush's work by polling an event: a flush is tens of microseconds of device
+  // work with the host idle meanwhile, and a blocking synchronisation's wake-up costs a large
+  // fraction of that.
+  void wait_stream()
+  {
+    check(hipEventRecord(done_, stream_), "hipEventRecord");
+    hipError_t e;
+    while ((e = hipEventQuery(done_)) == hipErrorNotReady) {
+    }
+    check(e, "hipEventQuery");
   }
 
   // Once per process, when the first encoder / decoder is made: pinned staging and a first
@@ -575,6 +593,7 @@ class Device {
   DevChunk* cur_ = nullptr;
   uint64_t epoch_ = 0;
   uint8_t *h_up_ = nullptr, *h_down_ = nullptr;   // pinned: flush uploads / results
+  hipEvent_t done_ = nullptr;                       // flush completion (wait_stream)
   size_t cap_up_ = 0, cap_down_ = 0;
 };
 
@@ -748,13 +767,17 @@ class Encoder {
       ++nb_sent_packets_;
       Pending p;
       p.enc = this;
-      begin(p, 7 + s.sym->size);
+      // with nothing of this encoder waiting in the batch, a source packet needs no GPU result:
+      // it goes out now, exactly as unbatched (the encoder's own sequence is unchanged)
+      const bool now = queued_ == 0;
+      if (now) out_.buf = nullptr;
+      else begin(p, 7 + s.sym->size);
       out_.u8(2);                                  // packetizer.hh:165-183
       out_.u32(s.id);
       out_.u16(s.sym->size);
       out_.raw(s.sym->data(), s.sym->size);
       out_.end();
-      finish(std::move(p));
+      if (!now) finish(std::move(p));
     } else {
       generate_repair();
     }
@@ -818,8 +841,9 @@ class Encoder {
   }
 
   void set_batch(Batch* b);
-  void drop_batch() { batch_ = nullptr; }
+  void drop_batch() { batch_ = nullptr; queued_ = 0; }
   Batch* batch() const { return batch_; }
+  size_t queued_ = 0;                  // this encoder's events waiting in its batch
   const ntc_packet_handler& handler() const { return out_.h; }
 
   // encoder.hh:290-318 + packetizer.hh:64-88 + source_list.hh:34-60
@@ -904,8 +928,9 @@ class Decoder {
   ~Decoder();
 
   void set_batch(Batch* b);
-  void drop_batch() { batch_ = nullptr; }
+  void drop_batch() { batch_ = nullptr; queued_ = 0; }
   const ntc_packet_handler& packet_handler() const { return out_.h; }
+  size_t queued_ = 0;                  // this decoder's events waiting in its batch
   const ntc_data_handler& data_handler() const { return dh_; }
 
   // decoder.hh:88-122.  own: the buffer p lies in, when the caller hands it over (the C ABI
@@ -949,13 +974,14 @@ class Decoder {
     Pending p;
     p.kind = Pending::DEC_PACKET;
     p.dec = this;
-    out_.buf = batch_ ? &p.pkt : nullptr;
+    const bool now = !batch_ || queued_ == 0;      // nothing of this decoder waiting: send now
+    out_.buf = now ? nullptr : &p.pkt;
     out_.u8(0);
     out_.u16(ack_packets_);
     out_.ids(ids);
     out_.end();
     out_.buf = nullptr;
-    queue(std::move(p));
+    if (!now) queue(std::move(p));
     ++nb_acks_;
     ack_packets_ = 0;
   }
@@ -1013,8 +1039,12 @@ class Decoder {
   // decoder.hh:231-248, 292-300
   void deliver(const Src& s)
   {
-    if (batch_) {
-      Pending p;                 // a received source's own payload, or a decoded one's value
+    if (batch_ && queued_ == 0 && s.node->has_value()) {
+      // nothing of this decoder waiting and the bytes are at hand (a received source): now
+      static const uint8_t zero[16] = {0};
+      dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.size ? s.node->data() : zero), s.size);
+    } else if (batch_) {
+      Pending p;                 // a decoded source's value, or anything behind a waiting event
       p.kind = Pending::DEC_DATA;
       p.dec = this;
       p.size = s.size;
@@ -1384,12 +1414,14 @@ class Batch {
   void attach(Decoder* d) { decs_.push_back(d); }
   void detach(Encoder* e)
   {
+    e->queued_ = 0;
     encs_.erase(std::remove(encs_.begin(), encs_.end(), e), encs_.end());
     q_.erase(std::remove_if(q_.begin(), q_.end(), [e](const Pending& p) { return p.enc == e; }),
              q_.end());
   }
   void detach(Decoder* d)
   {
+    d->queued_ = 0;
     decs_.erase(std::remove(decs_.begin(), decs_.end(), d), decs_.end());
     q_.erase(std::remove_if(q_.begin(), q_.end(), [d](const Pending& p) { return p.dec == d; }),
              q_.end());
@@ -1443,7 +1475,10 @@ void Encoder::begin(Pending& p, size_t reserve)
 void Encoder::finish(Pending&& p)
 {
   out_.buf = nullptr;
-  if (batch_) batch_->push(std::move(p));
+  if (batch_) {
+    batch_->push(std::move(p));
+    ++queued_;
+  }
 }
 
 Decoder::~Decoder()
@@ -1498,7 +1533,10 @@ void Decoder::set_batch(Batch* b)
 
 void Decoder::queue(Pending&& p)
 {
-  if (batch_) batch_->push(std::move(p));
+  if (batch_) {
+    batch_->push(std::move(p));
+    ++queued_;
+  }
 }
 
 Batch::~Batch()
@@ -1519,6 +1557,7 @@ void Batch::flush()
   q.swap(q_);
   if (q_.capacity() < spare_.capacity()) q_.swap(spare_);   // keep the queue's storage warm
   for (Pending& p : q) {
+    --(p.kind == Pending::ENC_PACKET ? p.enc->queued_ : p.dec->queued_);   // before its callback
     if (p.kind == Pending::DEC_DATA) {
       const ntc_data_handler& h = p.dec->data_handler();
       static const uint8_t zero[16] = {0};

@@ -8,6 +8,9 @@ timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout
 tail -1 gpurun_out/$TAG/pytest_gpu.log
 timeout -k 10 300 python bench.py > gpurun_out/$TAG/bench.log 2>&1 || { tail -20 gpurun_out/$TAG/bench.log; exit 1; }
 tail -1 gpurun_out/$TAG/bench.log
+# the driver's own command
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$TAG/bench_driver_cmd.log 2>&1 || { tail -20 gpurun_out/$TAG/bench_driver_cmd.log; exit 1; }
+tail -1 gpurun_out/$TAG/bench_driver_cmd.log | cut -c1-160
 export TMPDIR=/tmp
 OUT=$PWD/gpurun_out/$TAG
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- python3 $OLDPWD/bench.py --steps 10 --no-cpu-baseline --no-host-rate > $OUT/prof_bench.log 2>&1) || { tail -20 $OUT/prof_bench.log; exit 1; }

@@ -783,33 +783,33 @@ struct CoefWalk {
 // wave's LDS slice.  No block-wide barrier after the table copy.
 __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
 {
-  // LDS copy of the v_perm tables (encoded sizes).  Small generations (k * r < 1024) read the
-  // tables from the constant bank instead.
+  // LDS copy of the v_perm tables (encoded sizes), made only when some generation of the block
+  // has unequal source lengths (one product per source and row) and k * r >= 1024; otherwise
+  // the few lookups read the constant bank.
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
   __shared__ uint16_t part[4][256];
-  const bool lds_tabs = a.k * a.r >= 1024u;
-  if (lds_tabs) {                                 // uniform
-    const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
-    uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
-    for (uint32_t i = threadIdx.x; i < 512u; i += 256u) dst[i] = src[i];
-    __syncthreads();
-  }
-  const uint32_t (*tabs)[8] = lds_tabs ? ptab : d_perm.w;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t g = blockIdx.x * 4u + wv;
-  if (g >= a.G) return;
-  const uint32_t nw = a.rp >> 2;                  // rp % 4 == 0, rp <= 256: nw <= 64
-  const uint32_t nq = 64u / nw;                   // source slots
-  const uint32_t w = lane % nw, q = lane / nw;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * a.k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * a.r;
-  const uint16_t* len = a.src_len + static_cast<size_t>(g) * a.k;
-  uint16_t* pw = part[wv];
+  const bool live = g < a.G;
+  const uint16_t* len = a.src_len + static_cast<size_t>(live ? g : 0u) * a.k;
+  // id bases (and the pairing partner's) first: their loads overlap the length pass
+  const uint32_t sidb = a.sid_base ? a.sid_base[live ? g : 0u] : g * a.k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[live ? g : 0u] : g * a.r;
+  // pairing: a first-of-pair generation also walks its partner's coefficients and compares them
+  // (only when the partner's id bases are congruent mod 255, the necessary condition)
+  const bool first = live && a.pair && (g / kPairGap) % 2u == 0u;
+  const bool has_partner = first && g + kPairGap < a.G;
+  uint32_t psidb = 0, pridb = 0;
+  if (has_partner) {
+    const uint32_t gp = g + kPairGap;
+    psidb = a.sid_base ? a.sid_base[gp] : gp * a.k;
+    pridb = a.rid_base ? a.rid_base[gp] : gp * a.r;
+  }
   // source lengths: max (the repair length) and whether they are all equal -- then a repair's
   // encoded size is multiply_size(L, XOR of its coefficients) (the product distributes over XOR),
   // one product per repair instead of one per source
   uint32_t lmax = 0, lmin = 0xFFFFu;
-  for (uint32_t i = lane; i < a.k; i += 64u) {
+  for (uint32_t i = lane; live && i < a.k; i += 64u) {
     const uint32_t l = len[i];
     lmax = max(lmax, l);
     lmin = min(lmin, l);
@@ -819,17 +819,20 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
     lmax = max(lmax, static_cast<uint32_t>(__shfl_xor(lmax, o)));
     lmin = min(lmin, static_cast<uint32_t>(__shfl_xor(lmin, o)));
   }
-  const bool same_len = uniform(lmin) == uniform(lmax);
-  // pairing: a first-of-pair generation also walks its partner's coefficients and compares them
-  // (only when the partner's id bases are congruent mod 255, the necessary condition)
-  const bool first = a.pair && (g / kPairGap) % 2u == 0u;
-  const bool has_partner = first && g + kPairGap < a.G;
-  uint32_t psidb = 0, pridb = 0;
-  if (has_partner) {
-    const uint32_t gp = g + kPairGap;
-    psidb = a.sid_base ? a.sid_base[gp] : gp * a.k;
-    pridb = a.rid_base ? a.rid_base[gp] : gp * a.r;
+  const bool same_len = !live || uniform(lmin) == uniform(lmax);
+  const bool lds_tabs = __syncthreads_or(!same_len) && a.k * a.r >= 1024u;
+  if (lds_tabs) {                                 // uniform
+    const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
+    for (uint32_t i = threadIdx.x; i < 512u; i += 256u) dst[i] = src[i];
+    __syncthreads();
   }
+  const uint32_t (*tabs)[8] = lds_tabs ? ptab : d_perm.w;
+  if (!live) return;
+  const uint32_t nw = a.rp >> 2;                  // rp % 4 == 0, rp <= 256: nw <= 64
+  const uint32_t nq = 64u / nw;                   // source slots
+  const uint32_t w = lane % nw, q = lane / nw;
+  uint16_t* pw = part[wv];
   const bool cmp = has_partner && psidb % 255u == sidb % 255u && pridb % 255u == ridb % 255u;
   uint32_t diff = 0;
   if (q < nq) {

@@ -589,6 +589,8 @@ def kernel_summary(log, steps, dense):
             elif dense and name == "dense":
                 name = "dense_invert" if seen_dense else "dense_encode_layout"
                 seen_dense += 1
+            elif name == "other":                     # the split-k MAC's part reduction
+                name = "ksplit_reduce"
             tot[name] = tot.get(name, 0.0) + ms
             if name in launches:
                 launches[name].append(ms)

@@ -98,13 +98,16 @@ int  ntc_gf256_mac_time(ntc_gf256_engine* eng, int dec, float* ms);
  * microseconds that matter for sub-millisecond steps. */
 enum { NTC_GF256_K_ENCODE_PREP = 0, NTC_GF256_K_ENCODE_MAC = 1, NTC_GF256_K_DECODE_PLAN = 2,
        NTC_GF256_K_PLAN_ROWS = 3, NTC_GF256_K_DECODE_MAC = 4, NTC_GF256_K_BJ_OFFSETS = 5 /* reserved */,
-       NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 };
+       NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 /* the split-k MAC's part reduction */ };
 int  ntc_gf256_timing_log(ntc_gf256_engine* eng, uint32_t capacity);
 int  ntc_gf256_timing_kinds(ntc_gf256_engine* eng, uint32_t mask);
 int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uint32_t* kinds,
                            float* ms);
 
-/* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture). */
+/* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture).
+ * A bit-sliced encode / combine with fewer tasks than one round of wave slots (few generations,
+ * k >= 128) splits its sources (split-k) and sizes its partial outputs on first use: run such a
+ * call once before capturing it. */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
 
 /* Encode: rep[g][j] = sum_i c(rid_base[g]+j, sid_base[g]+i) * src[g][i] over GF(2^8)/0x11D.

@@ -25,6 +25,10 @@ struct ntc_gf256_engine {
   // 1 = shares its MAC wave with generation g + 255 (equal coefficient matrices), 2 = that partner
   void* enc_pair = nullptr;
   size_t enc_pair_cap = 0;
+  // split-k MAC partial outputs (launch_mac, few tasks) and the device's CU count
+  void* kout = nullptr;
+  size_t kout_cap = 0;
+  uint32_t ncu = 0;
   // the last plan also wrote the decode MAC's input row addresses (row_ptr) for these buffers
   const uint8_t* rows_src = nullptr;
   const uint8_t* rows_rep = nullptr;

@@ -19,6 +19,7 @@
 // (3-input XOR).  Sources are processed in pairs: 6 v_perm + 3 v_bitop3 per dword pair.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -168,6 +169,12 @@ struct MacArgs {
   uint32_t tile_fast;          // bit-sliced task order: 1 = row tile fastest, 0 = column span fastest
   const uint8_t* pair;         // encode pairing flags [G] (gf_mac_bs<.., PAIR>), see kPairGap
   uint64_t pair_in, pair_out;  // byte distance of the partner's sources / repairs
+  // split-k (bit-sliced encode / combine with less than one round of tasks): part ks sums the
+  // sources [ks * kpart, (ks + 1) * kpart) into out (ks = 0) or kout + (ks - 1) * kout_step, and
+  // ksplit_reduce folds the parts into out
+  uint32_t ksplit, kpart;
+  uint8_t* kout;
+  uint64_t kout_step;
 };
 
 // ---- hand-scheduled scalar loads -------------------------------------------------------------
@@ -459,7 +466,9 @@ template <> struct BsCoef<16> { using T = u32x4; };
 template <int R, bool DEC, bool FULL, bool PAIR = false>
 __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t tile,
                                         uint32_t nrows, uint32_t cc, uint32_t lane, uint32_t ring,
-                                        uint64_t poff_in = 0, uint64_t poff_out = 0)
+                                        uint64_t poff_in = 0, uint64_t poff_out = 0,
+                                        uint32_t i_begin = 0, uint32_t i_count = 0,
+                                        uint8_t* out_base = nullptr)
 {
   static_assert(R == 8 || R == 16, "8- or 16-row tiles");
   static_assert(!PAIR || (!DEC && !FULL), "pairing is an encode mode for short symbols");
@@ -467,7 +476,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   constexpr bool kLate = R == 16;
   using CoefV = typename BsCoef<R>::T;
   const size_t stride = a.stride;
-  const uint32_t k = a.k;
+  const uint32_t k = i_count ? i_count : a.k;           // sources this wave sums (split-k: a part)
   const uint32_t col = cc * 2048u;
   // One VGPR serves the LDS reads and the (FULL) DMA offsets: x = ring + 16*lane; the DMA's
   // scalar row base is pre-biased by col - ring.
@@ -475,10 +484,10 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   const bool v0 = FULL || col + lane * 16u < stride;
   const bool v1 = PAIR ? poff_out != 0 && v0 : FULL || col + lane * 16u + 1024u < stride;
   const uint32_t d0 = v0 ? x : ring, d1 = v1 ? (PAIR ? x : x + 1024u) : ring;   // !FULL DMA offsets
-  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
-  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
+  const uint8_t* base0 = a.in0 + (static_cast<size_t>(g) * a.k + i_begin) * stride;
+  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (a.k + kBsRing) : nullptr;
   const uint32_t jstep = a.rp;
-  const uint8_t* jp = a.coef + static_cast<size_t>(g) * k * a.rp + tile * R;
+  const uint8_t* jp = a.coef + (static_cast<size_t>(g) * a.k + i_begin) * a.rp + tile * R;
   const uint64_t bias = static_cast<uint64_t>(col) - ring;
   auto row_at = [&](uint32_t i) -> const uint8_t* {    // a scalar (SGPR) row address
     uint64_t v;
@@ -624,9 +633,9 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
     uint8_t* dst;
     if constexpr (DEC) {
       const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
-      dst = a.out + static_cast<size_t>(g) * k * stride + uniform(outs[j]) * stride;
+      dst = a.out + static_cast<size_t>(g) * a.k * stride + uniform(outs[j]) * stride;
     } else {
-      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
+      dst = (out_base ? out_base : a.out) + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
     }
     if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
     if (v1) *reinterpret_cast<uint4*>(dst + (PAIR ? poff_out + c0 : c1)) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
@@ -660,6 +669,11 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
     tile = task % a.nrowchunks;
     task /= a.nrowchunks;
   }
+  uint32_t ks = 0;
+  if (!DEC && !PAIR && a.ksplit > 1) {
+    ks = task % a.ksplit;
+    task /= a.ksplit;
+  }
   const uint32_t g = task;
   if (g >= a.G) return;
   const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
@@ -667,7 +681,11 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
   if (row0 >= total) return;
   const uint32_t nrows = min(static_cast<uint32_t>(R), total - row0);
   const uint32_t ring = lds_addr(s_ring + wave * (kBsRing * kBsSlot));
-  if constexpr (PAIR) {
+  if (!DEC && !PAIR && a.ksplit > 1) {
+    const uint32_t i0 = ks * a.kpart;                  // launch_mac: every part is non-empty
+    bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring, 0, 0, i0, min(a.kpart, a.k - i0),
+                          ks ? a.kout + (ks - 1) * a.kout_step : a.out);
+  } else if constexpr (PAIR) {
     const uint32_t pf = uniform(static_cast<uint32_t>(a.pair[g]));
     if (pf == 2) return;                               // encoded by its partner's wave
     bs_tile<R, DEC, FULL, true>(a, g, tile, nrows, cc, lane, ring, pf ? a.pair_in : 0, pf ? a.pair_out : 0);
@@ -2139,6 +2157,21 @@ mac_fn pick_bs(bool dec, uint32_t rowtile, bool full, bool pair)
              : (full ? gf_mac_bs<8, false, true> : gf_mac_bs<8, false, false>);
 }
 
+// out ^= the split-k parts 1 .. nparts (16 B per thread and step, grid-stride)
+__global__ __launch_bounds__(256) void ksplit_reduce(uint4* __restrict__ out, const uint4* __restrict__ parts,
+                                                     uint64_t n16, uint32_t nparts)
+{
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * 256u;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x; i < n16; i += step) {
+    uint4 v = out[i];
+    for (uint32_t p = 0; p < nparts; ++p) {
+      const uint4 w = parts[p * n16 + i];
+      v.x ^= w.x; v.y ^= w.y; v.z ^= w.z; v.w ^= w.w;
+    }
+    out[i] = v;
+  }
+}
+
 // Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
 int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what)
 {
@@ -2181,7 +2214,38 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   a.nrowchunks = (a.rows + rowtile - 1) / rowtile;
   a.ncolchunks = (a.stride + span - 1) / span;
   a.tile_fast = a.G < 64 ? 1u : 0u;
-  const uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
+  uint64_t tasks = static_cast<uint64_t>(a.G) * a.nrowchunks * a.ncolchunks;
+  // Split-k: a bit-sliced encode / combine with fewer 16-row tasks than one round of wave slots
+  // (3 per SIMD) -- dense n = 1024, G = 1: 2048 -- leaves SIMDs at 2 waves or fewer, each with a
+  // long source loop.  Splitting the sources into ksplit parts of >= 64 gives >= 8/3 rounds;
+  // the parts' partial repairs are XORed into out afterwards (ksplit_reduce, an HBM pass over
+  // ksplit + 1 copies of the output).
+  a.ksplit = 1;
+  a.kpart = a.k;
+  if (span == 2048 && !dec && !a.pair && rowtile == 16) {
+    if (!e->ncu) {
+      int n = 0;
+      if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || n <= 0) n = 256;
+      e->ncu = static_cast<uint32_t>(n);
+    }
+    const uint64_t slots = static_cast<uint64_t>(e->ncu) * 4u * 3u;
+    if (tasks < slots && a.k >= 128) {
+      // >= 8/3 rounds: measured at n = 1024 (2048 tasks), ksplit 2 / 3 / 4 / 6 / 8 -> MAC 1.01 /
+      // 0.93 / 0.90 / 0.93 / 0.90 ms, reduce 0.028 / 0.038 / 0.050 / 0.082 / 0.117 ms per call
+      uint32_t ks = static_cast<uint32_t>(std::min<uint64_t>((8 * slots + 3 * tasks - 1) / (3 * tasks), 8));
+      ks = std::min(ks, a.k / 64);
+      const uint32_t kpart = (a.k + ks - 1) / ks;
+      a.kpart = (kpart + 3) / 4 * 4;
+      a.ksplit = (a.k + a.kpart - 1) / a.kpart;          // every part non-empty
+    }
+  }
+  if (a.ksplit > 1) {
+    a.kout_step = static_cast<uint64_t>(a.G) * a.rows * a.stride;
+    int rc = ensure_buf(&e->kout, &e->kout_cap, (a.ksplit - 1) * a.kout_step, "hipMalloc split-k parts");
+    if (rc) return rc;
+    a.kout = static_cast<uint8_t*>(e->kout);
+    tasks *= a.ksplit;
+  }
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
@@ -2190,8 +2254,18 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     hipExtLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, kt.start(),
                           kt.stop(), 0, a);
   }
+  int rc = hip_check(hipGetLastError(), what);
+  if (!rc && a.ksplit > 1) {
+    const uint64_t n16 = a.kout_step / 16;               // stride % 16 == 0
+    const uint32_t nblk = static_cast<uint32_t>(std::min<uint64_t>((n16 + 255) / 256, 8192));
+    KernelTimer kt(e, NTC_GF256_K_OTHER, st, true);
+    hipExtLaunchKernelGGL(ksplit_reduce, dim3(nblk), dim3(256), 0, st, kt.start(), kt.stop(), 0,
+                          reinterpret_cast<uint4*>(a.out), reinterpret_cast<const uint4*>(a.kout), n16,
+                          a.ksplit - 1);
+    rc = hip_check(hipGetLastError(), "ksplit_reduce launch");
+  }
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][1], st);
-  return hip_check(hipGetLastError(), what);
+  return rc;
 }
 
 }  // namespace
@@ -2309,6 +2383,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->plan_coef);
   (void)hipFree(e->enc_coef);
   (void)hipFree(e->enc_pair);
+  (void)hipFree(e->kout);
   (void)hipFree(e->row_ptr);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   for (auto& pair : e->mac_ev)

@@ -94,6 +94,10 @@ ENCODE_CASES = [
     # lean-loop MAC (full 2 KiB spans, k % 4 == 0): only the final group of 4 sources; 3 spans
     (5, 4, 3, 2048, 2048, True, "offset"),
     (3, 12, 9, 6144, 6144, True, "wrap"),
+    # split-k (few tasks, k >= 128): parts of 68 sources and a short last part, partial outputs
+    # XORed by ksplit_reduce; ragged spans, 16 + 4 row tiles
+    (2, 203, 20, 2080, 2080, True, "offset"),
+    (3, 130, 17, 4096, 4096, False, "wrap"),
     # generation pairing (continuous ids, stride <= 1024, G > 255): g and g + 255 share one MAC
     # wave when their matrices match; a tail of unpaired generations; odd row tiles; half fill
     (700, 32, 8, 1024, 1024, True, "default"),

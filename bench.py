@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-rate", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--mac", default="auto", choices=("auto", "perm", "bitslice"),
+                   help="region-MAC formulation (exploration; the line records it when not auto)")
     pp = p.add_argument_group("per-packet drop-in comparison (--per-packet)")
     pp.add_argument("--per-packet", action="store_true")
     pp.add_argument("--flows", type=int, default=256)
@@ -658,6 +660,8 @@ def main():
     else:
         w = Workload(dev, G, k, r, S, stride, m, a.mixed, rank)
         engine = w.enc.engine
+    if a.mac != "auto":
+        engine.set_mac_kind(a.mac)
 
     # optional: the HBM copy probe (reported in the roofline) before the warmup steps, with more
     # repetitions (clock ramp experiment, NTC_BENCH_PROBE_FIRST=<reps>)
@@ -745,7 +749,8 @@ def main():
             "data": "synthetic (seeded random payloads, exact-m uniform loss)",
             "config": {"workload": a.config, "k": k, "r": r, "S": S, "stride": stride,
                        "m": ("U[0,%d]" % m) if a.mixed else m, "generations_per_gpu": G,
-                       "parallelism": f"generation-shard x{world} (no collectives)"},
+                       "parallelism": f"generation-shard x{world} (no collectives)",
+                       **({"mac": a.mac} if a.mac != "auto" else {})},
             "value_note": "G*k*S source-payload bytes per step over all G generations; "
                           f"{G - ndec} of {G} per rank are singular under the reference "
                           "coefficient schedule (encoded and planned, no decode MAC)",

@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-rate", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--graph", action="store_true",
+                   help="replay the step from a captured HIP graph (exploration; recorded in the line)")
     p.add_argument("--mac", default="auto", choices=("auto", "perm", "bitslice"),
                    help="region-MAC formulation (exploration; the line records it when not auto)")
     pp = p.add_argument_group("per-packet drop-in comparison (--per-packet)")
@@ -668,10 +670,26 @@ def main():
     probe_reps = int(os.environ.get("NTC_BENCH_PROBE_FIRST", "0"))
     probe = hbm_copy_probe(dev, reps=probe_reps) if probe_reps else None
     nprof = min(a.steps, 10)
+    step = w.step
+    if a.graph:
+        # the whole step (every launch of encode + decode) captured once, replayed per step: the
+        # same kernels on the same buffers, only the per-launch host and dispatch cost goes
+        s_cap = torch.cuda.Stream(dev)
+        s_cap.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s_cap):
+            for _ in range(2):
+                w.step()
+        torch.cuda.current_stream(dev).wait_stream(s_cap)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            w.step()
+        torch.cuda.synchronize(dev)
+        step = graph.replay
     engine.timing_log(nprof * 16)        # the log's events exist before the clock starts ...
     engine.timing_kinds(())              # ... but nothing is logged until the profiled steps
     for _ in range(a.warmup):
-        w.step()
+        step()
     torch.cuda.synchronize(dev)
 
     def barrier():
@@ -685,7 +703,7 @@ def main():
     # 12-15 % of a config-2 step, so `value` is measured without them
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        w.step()
+        step()
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -750,7 +768,8 @@ def main():
             "config": {"workload": a.config, "k": k, "r": r, "S": S, "stride": stride,
                        "m": ("U[0,%d]" % m) if a.mixed else m, "generations_per_gpu": G,
                        "parallelism": f"generation-shard x{world} (no collectives)",
-                       **({"mac": a.mac} if a.mac != "auto" else {})},
+                       **({"mac": a.mac} if a.mac != "auto" else {}),
+                       **({"step": "HIP graph replay"} if a.graph else {})},
             "value_note": "G*k*S source-payload bytes per step over all G generations; "
                           f"{G - ndec} of {G} per rank are singular under the reference "
                           "coefficient schedule (encoded and planned, no decode MAC)",

@@ -707,6 +707,9 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
+    # graph mode: the replayed steps' own outputs are checked too (the profiled steps below run
+    # eagerly, with per-launch events)
+    graph_good = w.verify()[0] if a.graph else None
     # profiled steps straight after (no host work in between, so the clocks stay where the timed
     # steps left them): every kernel launch timed by the event pair its dispatch stamps (engine
     # timing log, hipExtLaunchKernelGGL), so the per-kernel breakdown and the roofline kernel's
@@ -781,7 +784,8 @@ def main():
             "ms_per_step_profiled": round(ms_prof, 4),
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_prof),
-            "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good}}
+            "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good,
+                         **({"graph_replay_bit_exact": graph_good} if a.graph else {})}}
     if rank == 0 and world == 1 and not a.no_host_rate:
         hk, hp, hs, hok = host_rate(w)
         line["host_resident_GiBps"] = round(hk, 3)
@@ -801,7 +805,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
-    if not good:
+    if not good or graph_good is False:
         sys.exit(3)
 
 

@@ -6,7 +6,8 @@ m lost sources each (received sources + repairs -> recovered sources), all buffe
 HBM.  value = G*k*S payload bytes per step / step time (GiB/s), aggregated over ranks.
 
 Multi-GPU (torchrun): every rank owns G independent generations with its own id range (weak
-scaling, no data-path collective); only a barrier and a max-reduce of the timing use RCCL.
+scaling, no data-path collective); only a barrier and a max-reduce of the timing cross ranks, over
+gloo (host tensors): no RCCL initialisation is needed for the N-GPU launch.
 
 Extras in the JSON line:
 * the timed steps run bare (no events: timing every launch costs 1.5 % of a config-3 step and
@@ -130,6 +131,46 @@ class Workload:
         self.dec(self.rx, self.rx_len, self.smask, self.out.repairs, self.out.encoded_size,
                  self.rmask, self.sid, self.rid, self.status)
 
+    POISON = 0xA5
+
+    def poison(self):
+        """Before the last profiled step: every output of the step is overwritten with a poison
+        byte -- the lost source slots (the decoder's in-place outputs), the repairs, the encoded
+        sizes, the status words -- after keeping the previous step's repairs / sizes / status.
+        Steps are deterministic, so after the step `rewritten()` proves the step recomputed all
+        of them (a skipped or partial launch would leave poison behind)."""
+        self._prev = (self.out.repairs.clone(), self.out.encoded_size.clone(), self.status.clone())
+        self.rx[self.smask == 0] = self.POISON
+        self.out.repairs.fill_(self.POISON)
+        self.out.encoded_size.fill_(-23131)            # 0xA5A5
+        self.status.fill_(self.POISON)
+
+    def rewritten(self):
+        rep, esz, st = self._prev
+        from netcode_amd import status_to_numpy
+        dec = torch.from_numpy(status_to_numpy(self.status)["state"] == 0).to(self.dev)
+        lost = (self.smask == 0) & dec[:, None]
+        ok = (torch.equal(self.out.repairs, rep) and torch.equal(self.out.encoded_size, esz) and
+              torch.equal(self.status, st) and bool((self.rx[lost] == self.src[lost]).all()))
+        self._prev = None
+        return ok
+
+    def oracle_sample(self, n=24, n_singular=8):
+        """Host copies of a sample of generations of the last step (evenly spaced + the first
+        singular ones), for the oracle comparison of the cpu_baseline leg."""
+        from netcode_amd import status_to_numpy
+        st = status_to_numpy(self.status)
+        g = set(np.linspace(0, self.G - 1, min(n, self.G)).astype(int).tolist())
+        g |= set(np.nonzero(st["state"] == 3)[0][:n_singular].tolist())
+        g = np.array(sorted(g))
+        gi = torch.from_numpy(g).to(self.dev)
+        h = lambda t: t.index_select(0, gi).cpu().numpy()
+        return {"g": g, "src": h(self.src), "len": h(self.src_len).view(np.uint16),
+                "mask": h(self.smask), "rmask": h(self.rmask), "sid": h(self.sid).view(np.uint32),
+                "rid": h(self.rid).view(np.uint32), "rep": h(self.out.repairs),
+                "esz": h(self.out.encoded_size).view(np.uint16), "rx": h(self.rx),
+                "rx_len": h(self.rx_len).view(np.uint16), "status": st[g], "k": self.k, "r": self.r}
+
     def verify(self):
         """(bit-exact, decoded generations, decode MAC bytes, decode byte-MACs) of the last step.
         Every generation with a loss must end decoded or singular (all repairs arrive and m <= r,
@@ -171,6 +212,22 @@ class DenseWorkload:
         self.rep = torch.empty((G, k, S), dtype=torch.uint8, device=dev)
         self.out = torch.empty_like(self.src)
         self.ok = torch.empty((G,), dtype=torch.uint8, device=dev)
+
+    def poison(self):
+        """Before the last profiled step: the decoded-source buffer and the repairs are poisoned
+        (after keeping the previous step's repairs); see Workload.poison."""
+        self._prev = self.rep.clone()
+        self.out.fill_(0xA5)
+        self.rep.fill_(0xA5)
+        self.ok.fill_(0)
+
+    def rewritten(self):
+        ok = torch.equal(self.rep, self._prev) and torch.equal(self.out, self.src)
+        self._prev = None
+        return ok
+
+    def oracle_sample(self):
+        return None
 
     def step(self):
         self.dc.encode(self.mat, self.src, self.rep)
@@ -539,6 +596,30 @@ def per_packet_main(a):
         sys.exit(3)
 
 
+def oracle_check(smp, threads):
+    """cpu_baseline leg (the oracle is the checker here, never the measured path): the sampled
+    generations of the bench's own last step against the oracle on the same sources, lengths, id
+    bases and loss masks -- repairs, encoded sizes, per-generation decode status, recovered slots
+    and lengths, bit for bit."""
+    from oracle import oracle as O
+    k, r = smp["k"], smp["r"]
+    orep, orsz = O.encode_batch(smp["src"], smp["len"], k, r, smp["sid"], smp["rid"], simd=True,
+                                threads=threads)
+    lost = smp["src"] * smp["mask"][:, :, None]
+    out, olen, ost = O.decode_batch(lost, smp["len"] * smp["mask"], smp["mask"], orep, orsz,
+                                    smp["rmask"], smp["sid"], smp["rid"], threads=threads)
+    # slots the decoder owns: every slot of a decoded generation, the received ones otherwise (the
+    # lost slots of a generation that does not decode are not written by either side)
+    own = (ost["state"] == 0)[:, None] | (smp["mask"] != 0)
+    res = {"repairs": bool((orep == smp["rep"]).all()), "encoded_sizes": bool((orsz == smp["esz"]).all()),
+           "status": bool((ost == smp["status"]).all()),
+           "decoded_slots": bool((out[own] == smp["rx"][own]).all()),
+           "decoded_lengths": bool((olen == smp["rx_len"]).all()),
+           "decoded_generations": int((ost["state"] == 0).sum()),
+           "singular_generations": int((ost["state"] == 3).sum())}
+    return all(v for k_, v in res.items() if isinstance(v, bool)), res
+
+
 def cpu_baseline_dense(w, sample_bytes=1024):
     """Config 5 CPU leg: the oracle's dense encode (region MACs, AVX2 split-nibble) and dense
     decode (the reference's jerasure-order Gauss-Jordan, invert_matrix.cc:9-128, then the MACs
@@ -629,9 +710,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; NTC_BENCH_BACKEND=gloo lets a test run several ranks on fewer GPUs
-    # (ranks then share devices round-robin), RCCL ("nccl") otherwise
-    backend = os.environ.get("NTC_BENCH_BACKEND", "nccl")
+    # one process per GPU.  The ranks exchange no data: the barrier and the step-time
+    # max run over gloo on host tensors, so the N-GPU launch never initialises RCCL
+    # (NTC_BENCH_BACKEND=nccl selects it).  With fewer GPUs than ranks (a test), ranks share
+    # devices round-robin.
+    backend = os.environ.get("NTC_BENCH_BACKEND", "gloo")
     ndev = torch.cuda.device_count()
     local = local % ndev if (backend == "gloo" and ndev) else local
     if world > 1:
@@ -716,15 +799,24 @@ def main():
     # duration come from these launches, checked against these steps' own wall time
     engine.timing_kinds(None)
     tp = time.perf_counter()
-    for _ in range(nprof):
+    for _ in range(nprof - 1):
         w.step()
     torch.cuda.synchronize(dev)
-    ms_prof = (time.perf_counter() - tp) / nprof * 1e3
+    ms_prof = (time.perf_counter() - tp) * 1e3
+    w.poison()                           # outside the profiled clock, inside the event log
+    torch.cuda.synchronize(dev)
+    tp = time.perf_counter()
+    w.step()
+    torch.cuda.synchronize(dev)
+    ms_prof = (ms_prof + (time.perf_counter() - tp) * 1e3) / nprof
     log = engine.timing_read()
     engine.timing_log(0)
+    rewritten = w.rewritten()
     # outputs of the last step (the same computation as every timed step), checked after the
     # clocks stop
     good, ndec, dec_bytes, dec_macs = w.verify()
+    good = good and rewritten
+    smp = w.oracle_sample() if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
     if world > 1:
         import torch.distributed as dist
         from netcode_amd.shard import max_over_ranks
@@ -764,6 +856,7 @@ def main():
 
     line = {"metric": metric_name(a.config, k, r, S),
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": n_gpus, "ranks": world,
+            "rank_sync": backend if world > 1 else None,
             "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8 (GF(2^8))",
@@ -785,6 +878,10 @@ def main():
             "kernel_sum_ms_per_step": round(ksum, 4),
             "kernels_fit_in_step": bool(ksum <= ms_prof),
             "verified": {"decoded_generations": ndec, "bit_exact_round_trip": good,
+                         "poisoned_slots_rewritten": rewritten,
+                         "poison_note": "before the last profiled step every output (lost slots, "
+                                        "repairs, encoded sizes, status) was overwritten with 0xA5; "
+                                        "after it all equal the previous step's / the sources",
                          **({"graph_replay_bit_exact": graph_good} if a.graph else {})}}
     if rank == 0 and world == 1 and not a.no_host_rate:
         hk, hp, hs, hok = host_rate(w)
@@ -800,6 +897,14 @@ def main():
         thr = a.cpu_threads or usable          # every CPU this process may run on
         line["cpu_baseline"] = (cpu_baseline_dense(w) if dense
                                 else cpu_baseline(k, r, S, stride, m, thr))
+        if smp is not None:
+            ok, parts = oracle_check(smp, thr)
+            line["verified"]["oracle_slice_bit_exact"] = ok
+            line["verified"]["oracle_slice"] = {
+                "generations": [int(x) for x in smp["g"]], "checked": parts,
+                "how": "the bench's own last-step outputs of these generations vs or_encode_batch / "
+                       "or_decode_batch on the same sources, ids and masks (cpu_baseline leg)"}
+            good = good and ok
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -23,10 +23,7 @@ size_t ntc_encoder_counter(const ntc_encoder_t* enc, int which) NTC_C_NOEXCEPT N
 size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT NTC_C_NONNULL;
 
 /* Online batching adaptor.  Encoders and decoders attached to a batch queue
- * the packets and data deliveries that need a GF result (encoder repairs, decoded sources) -- and
- * everything an object produces after one of its events is queued -- instead of calling their
- * handlers; an event of an object with nothing queued that needs no GF result (a source packet, a
- * received source's delivery, an ack) is emitted at once.  Protocol state (windows, rates,
+ * every packet and data delivery they produce instead of calling their handlers.  Protocol state (windows, rates,
  * counters, missing / pending sets, acks) advances immediately -- the reference's control flow
  * never depends on payload bytes -- while each GF region result is kept as a linear expression
  * over the payloads it came from.  ntc_batch_flush evaluates every pending expression with one
@@ -34,7 +31,11 @@ size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT N
  * handlers in production order (a queued packet as one prepare_packet call followed by
  * send_packet).  Each object's callback sequence is byte-for-byte the unbatched one
  * (encoder.hh:255-333, decoder.hh:88-300 semantics); only the time of some callbacks moves to the
- * flush.  Attaching an object to another batch or to NULL flushes its current batch first.
+ * flush.  Eager mode (ntc_batch_set_eager, off by default) emits an event that needs no GF result
+ * (a source packet, a received source's delivery, an ack) of an object with nothing queued at
+ * once, inside the call that produced it: callbacks then run both there and at the flush, so a
+ * handler must be re-entrant with respect to the objects of the same batch.  Attaching an object
+ * to another batch or to NULL flushes its current batch first.
  * Deleting an attached object discards its queued events; deleting a batch discards every queued
  * event and detaches its objects. */
 typedef struct ntc_batch_t ntc_batch_t;
@@ -44,6 +45,7 @@ void ntc_encoder_set_batch(ntc_encoder_t* enc, ntc_batch_t* batch, ntc_error* er
 void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT;
 void ntc_batch_flush(ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT NTC_C_NONNULL;
 size_t ntc_batch_pending(const ntc_batch_t* batch) NTC_C_NOEXCEPT NTC_C_NONNULL;
+void ntc_batch_set_eager(ntc_batch_t* batch, int on) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 
 /* GF(2^w) region work on host buffers, run on the MI355X engine (one H2D, one combine launch,
  * one D2H): the region operations of the C++ detail layer (include/netcode/detail/galois_field.hh,

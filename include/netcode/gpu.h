@@ -106,11 +106,12 @@ int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uin
 
 /* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture).
  * A bit-sliced encode / combine with fewer tasks than one round of wave slots (few generations,
- * k >= 128) splits its sources (split-k) and sizes its partial outputs on first use: run such a
- * call once before capturing it. */
+ * k >= 128) splits its sources (split-k) and sizes its partial outputs on first use; a call
+ * captured before that first use runs unsplit instead of allocating (identical results). */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
 
 /* Encode: rep[g][j] = sum_i c(rid_base[g]+j, sid_base[g]+i) * src[g][i] over GF(2^8)/0x11D.
+ * Any r (the coefficient walk runs in chunks of 256 rows); k <= 65535.
  * rep_size[g][j] = encoded size (XOR of bytewise-coded u16 lengths); rep_len[g] = repair symbol
  * length = max src_len over the generation (may be NULL). */
 int  ntc_gf256_encode_batch(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r,

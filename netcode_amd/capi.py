@@ -83,7 +83,7 @@ def load():
         "ntc_new_batch": (P, []), "ntc_delete_batch": (None, [P]),
         "ntc_encoder_set_batch": (None, [P, P, E]), "ntc_decoder_set_batch": (None, [P, P, E]),
         "ntc_batch_flush": (None, [P, E]),
-        "ntc_batch_pending": (S, [P]),
+        "ntc_batch_pending": (S, [P]), "ntc_batch_set_eager": (None, [P, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -109,9 +109,14 @@ class _Collector:
         self._s = SEND(self._end)
         self.handler = PacketHandler(None, self._p, self._s)
 
+        self.on_packet = None         # optional hook, called with each finished packet
+
     def _end(self, ctx):
-        self.packets.append(bytes(self._cur))
+        pkt = bytes(self._cur)
+        self.packets.append(pkt)
         self._cur = bytearray()
+        if self.on_packet is not None:
+            self.on_packet(pkt)
 
 
 def _packet(L, pkt: bytes):
@@ -193,11 +198,13 @@ class Batch:
     """ntc_batch_t (netcode/c/ext.h): attached encoders' packets are queued until flush(), which
     computes every pending repair in one GPU launch per field size and emits in production order."""
 
-    def __init__(self):
+    def __init__(self, eager: bool = False):
         self.L = load()
         self.h = self.L.ntc_new_batch()
         if not self.h:
             raise MemoryError
+        if eager:
+            self.L.ntc_batch_set_eager(self.h, 1)
 
     def flush(self):
         err = Error(0, None)

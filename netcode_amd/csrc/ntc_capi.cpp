@@ -511,11 +511,18 @@ class Device {
   // Wait for the flush's work by polling an event: a flush is tens of microseconds of device
   // work with the host idle meanwhile, and a blocking synchronisation's wake-up costs a large
   // fraction of that.
+  // Spin on the event for at most ~50 us (a flush's usual length), then block in
+  // hipEventSynchronize: a long flush does not burn a core while other threads wait on mu_.
   void wait_stream()
   {
     check(hipEventRecord(done_, stream_), "hipEventRecord");
     hipError_t e;
+    const auto t0 = std::chrono::steady_clock::now();
     while ((e = hipEventQuery(done_)) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
+        check(hipEventSynchronize(done_), "hipEventSynchronize");
+        return;
+      }
     }
     check(e, "hipEventQuery");
   }
@@ -767,9 +774,9 @@ class Encoder {
       ++nb_sent_packets_;
       Pending p;
       p.enc = this;
-      // with nothing of this encoder waiting in the batch, a source packet needs no GPU result:
-      // it goes out now, exactly as unbatched (the encoder's own sequence is unchanged)
-      const bool now = queued_ == 0;
+      // unbatched, or an eager batch with nothing of this encoder waiting: a source packet needs
+      // no GPU result, so it goes out now (the encoder's own sequence is unchanged)
+      const bool now = emit_now();
       if (now) out_.buf = nullptr;
       else begin(p, 7 + s.sym->size);
       out_.u8(2);                                  // packetizer.hh:165-183
@@ -843,6 +850,7 @@ class Encoder {
   void set_batch(Batch* b);
   void drop_batch() { batch_ = nullptr; queued_ = 0; }
   Batch* batch() const { return batch_; }
+  bool emit_now() const;               // an event needing no GF result goes out at once
   size_t queued_ = 0;                  // this encoder's events waiting in its batch
   const ntc_packet_handler& handler() const { return out_.h; }
 
@@ -974,7 +982,7 @@ class Decoder {
     Pending p;
     p.kind = Pending::DEC_PACKET;
     p.dec = this;
-    const bool now = !batch_ || queued_ == 0;      // nothing of this decoder waiting: send now
+    const bool now = emit_now();                   // unbatched, or eager with nothing waiting
     out_.buf = now ? nullptr : &p.pkt;
     out_.u8(0);
     out_.u16(ack_packets_);
@@ -1021,6 +1029,9 @@ class Decoder {
   };
 
   void queue(Pending&& p);
+ public:
+  bool emit_now() const;
+ private:
   // batch mode: the reduced repair as one payload (its own payload when nothing was removed)
   NodeRef repair_node(const Rep& r) const
   {
@@ -1039,8 +1050,8 @@ class Decoder {
   // decoder.hh:231-248, 292-300
   void deliver(const Src& s)
   {
-    if (batch_ && queued_ == 0 && s.node->has_value()) {
-      // nothing of this decoder waiting and the bytes are at hand (a received source): now
+    if (batch_ && emit_now() && s.node->has_value()) {
+      // an eager batch, nothing of this decoder waiting, the bytes at hand (a received source)
       static const uint8_t zero[16] = {0};
       dh_.read_data(dh_.context, reinterpret_cast<const char*>(s.size ? s.node->data() : zero), s.size);
     } else if (batch_) {
@@ -1438,6 +1449,10 @@ class Batch {
   }
   size_t pending() const { return q_.size(); }
   void flush();
+  // Eager emission (opt-in, ntc_batch_set_eager): an event that needs no GF result -- a source
+  // packet, a received source's delivery, an ack -- of an object with nothing queued goes out at
+  // once instead of at the flush.
+  bool eager = false;
 
  private:
   std::vector<Encoder*> encs_;
@@ -1446,6 +1461,9 @@ class Batch {
   std::vector<Pending> spare_;   // the last flushed queue's storage, reused by the next one
   std::vector<bytes> pool_;      // flushed packets' buffers (no malloc / free per packet)
 };
+
+bool Encoder::emit_now() const { return !batch_ || (batch_->eager && queued_ == 0); }
+bool Decoder::emit_now() const { return !batch_ || (batch_->eager && queued_ == 0); }
 
 Encoder::~Encoder()
 {
@@ -1739,6 +1757,11 @@ void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* b, ntc_error* error)
 {
   ntcx::guarded([&] { dec->d.set_batch(b ? &b->b : nullptr); }, error);
 }
+void ntc_batch_set_eager(ntc_batch_t* b, int on) noexcept
+{
+  if (b) b->b.eager = on != 0;
+}
+
 void ntc_batch_flush(ntc_batch_t* b, ntc_error* error) noexcept
 {
   ntcx::guarded([&] { b->b.flush(); }, error);

@@ -847,12 +847,16 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
   }
   const uint32_t (*tabs)[8] = lds_tabs ? ptab : d_perm.w;
   if (!live) return;
-  const uint32_t nw = a.rp >> 2;                  // rp % 4 == 0, rp <= 256: nw <= 64
-  const uint32_t nq = 64u / nw;                   // source slots
-  const uint32_t w = lane % nw, q = lane / nw;
   uint16_t* pw = part[wv];
   const bool cmp = has_partner && psidb % 255u == sidb % 255u && pridb % 255u == ridb % 255u;
   uint32_t diff = 0;
+  // Rows go in chunks of at most 256 (64 coefficient words): one chunk whenever r <= 256.
+  const uint32_t nwt = a.rp >> 2;                 // rp % 4 == 0
+  for (uint32_t wb = 0; wb < nwt; wb += 64u) {
+  const uint32_t nw = min(nwt - wb, 64u);
+  const uint32_t nq = 64u / nw;                   // source slots
+  const uint32_t w = wb + lane % nw, q = lane / nw;
+  const uint32_t cr = 4u * nw;                    // this chunk's rows: [4 * wb, 4 * wb + cr)
   if (q < nq) {
     uint8_t* coef = a.coef + static_cast<size_t>(g) * a.k * a.rp + 4u * w;
     CoefWalk cw[4] = {CoefWalk(ridb + 4u * w + 1u, sidb + q + 1u, nq),
@@ -898,7 +902,20 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
       for (uint32_t b = 0; b < 4; ++b) esz[b] = mul4(tabs[(csum >> (8 * b)) & 0xFFu], lmax);
     }
 #pragma unroll
-    for (uint32_t b = 0; b < 4; ++b) pw[q * a.rp + 4u * w + b] = static_cast<uint16_t>(esz[b]);
+    for (uint32_t b = 0; b < 4; ++b) pw[q * cr + 4u * (w - wb) + b] = static_cast<uint16_t>(esz[b]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // pw holds nq * cr <= 256 partial sizes
+  for (uint32_t j = lane; j < cr && 4u * wb + j < a.r; j += 64u) {
+    uint16_t e = 0;
+    for (uint32_t s2 = 0; s2 < nq; ++s2) e ^= pw[s2 * cr + j];
+    a.rep_size[static_cast<size_t>(g) * a.r + 4u * wb + j] = e;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();                // the next chunk reuses pw
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (first) {
     const bool same = cmp && __ballot(diff != 0) == 0;
@@ -906,15 +923,6 @@ __global__ __launch_bounds__(256) void encode_prep(PrepArgs a)
       a.pair[g] = same ? 1 : 0;
       if (has_partner) a.pair[g + kPairGap] = same ? 2 : 0;
     }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // pw holds nq * rp <= 256 partial sizes
-  for (uint32_t j = lane; j < a.r; j += 64u) {
-    uint16_t e = 0;
-    for (uint32_t s2 = 0; s2 < nq; ++s2) e ^= pw[s2 * a.rp + j];
-    a.rep_size[static_cast<size_t>(g) * a.r + j] = e;
   }
   if (a.rep_len && lane == 0) a.rep_len[g] = static_cast<uint16_t>(lmax);   // max source length
 }
@@ -2241,6 +2249,16 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   }
   if (a.ksplit > 1) {
     a.kout_step = static_cast<uint64_t>(a.G) * a.rows * a.stride;
+    // a stream being captured into a graph must not allocate: without room for the parts, run
+    // unsplit (same results; ntc_gf256_reserve cannot size this buffer, it knows no stride)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if ((a.ksplit - 1) * a.kout_step > e->kout_cap && hipStreamIsCapturing(st, &cap) == hipSuccess &&
+        cap != hipStreamCaptureStatusNone) {
+      a.ksplit = 1;
+      a.kpart = a.k;
+    }
+  }
+  if (a.ksplit > 1) {
     int rc = ensure_buf(&e->kout, &e->kout_cap, (a.ksplit - 1) * a.kout_step, "hipMalloc split-k parts");
     if (rc) return rc;
     a.kout = static_cast<uint8_t*>(e->kout);
@@ -2511,10 +2529,14 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   if (rc) return rc;
   // generation pairing (kPairGap): symbols of at most half a bit-sliced span that fill at least a
-  // third of it when paired; pays off with continuous ids
+  // third of it when paired; pays off with continuous ids.  Under AUTO, a stride the unpaired
+  // bit-sliced kernel would not take (< 1/3 of a span) pairs only with the default continuous
+  // ids: explicit id bases may leave every generation unpaired, and an unpaired PAIR wave runs
+  // half its lanes idle where the v_perm MAC would have been chosen.
   const bool pairing = G > kPairGap && stride <= 1024 &&
                        (e->mac_kind == NTC_GF256_MAC_BITSLICE ||
-                        (e->mac_kind == NTC_GF256_MAC_AUTO && 2u * stride * 100u >= 2048u * 33u));
+                        (e->mac_kind == NTC_GF256_MAC_AUTO && 2u * stride * 100u >= 2048u * 33u &&
+                         (use_bitslice(e, stride) || (!sid_base && !rid_base))));
   if (pairing &&
       (rc = ensure_buf(&e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair")))
     return rc;

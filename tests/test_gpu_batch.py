@@ -85,9 +85,8 @@ def test_detach_flushes_and_delete_discards(capi):
         d = bytes([i]) * (10 + i)
         for e in (a, b, c):
             e.add_data(d)
-    # a's packets up to its first repair went out at once (nothing of a was waiting); the rest
-    # wait behind that repair
-    assert a.packets == b.packets[:len(a.packets)] and len(a.packets) < len(b.packets)
+    # deferred (the default): nothing of a goes out before the flush
+    assert a.packets == [] and len(b.packets) > 0
     assert batch.pending > 0
     a.set_batch(None)                 # flushes the batch: a (and c) catch up
     assert a.packets == b.packets and c.packets == b.packets
@@ -174,5 +173,52 @@ def test_batch_switching_and_shared_batch(capi, oracle):
         if step == 90:
             da.set_batch(None)             # flush + materialise; immediate from here on
     batch.flush()
+    assert da.data == db.data and da.packets == db.packets
+    assert db.nb_decoded > 0
+
+
+def test_eager_batch_emits_early_and_reenters(capi):
+    """Eager mode (ntc_batch_set_eager): a source packet of an encoder with nothing queued goes out
+    inside add_data; the packet handler re-enters a decoder attached to the SAME batch (its
+    deliveries and acks are produced during the encoder's call).  Every object's sequence still
+    equals its unbatched twin's."""
+    batch = capi.Batch(eager=True)
+    ea, eb = capi.Encoder(), capi.Encoder()
+    da, db = capi.Decoder(in_order=True), capi.Decoder(in_order=True)
+    for e in (ea, eb):
+        e.set_rate(3)
+    for d in (da, db):
+        d.set_ack_period_ms(0)
+        d.set_ack_nb_packets(7)
+    ea.set_batch(batch)
+    da.set_batch(batch)
+    rng = np.random.default_rng(5)
+    drop = set(int(i) for i in rng.choice(400, 60, replace=False))
+    seen = {"a": 0, "b": 0}
+
+    def feed(tag, dec):
+        def on_packet(pkt):
+            i = seen[tag]
+            seen[tag] += 1
+            if i not in drop:
+                dec.add_packet(pkt)       # re-entrant: the decoder shares ea's batch
+        return on_packet
+
+    ea._out.on_packet = feed("a", da)
+    eb._out.on_packet = feed("b", db)
+    early = 0
+    for step in range(200):
+        data = rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8).tobytes()
+        n0 = len(ea.packets)
+        ea.add_data(data)
+        eb.add_data(data)
+        early += len(ea.packets) > n0
+        if step % 9 == 8:
+            batch.flush()
+            assert ea.packets == eb.packets
+            assert da.data == db.data and da.packets == db.packets
+    batch.flush()
+    assert early > 0                      # eager: some packets left inside add_data
+    assert ea.packets == eb.packets
     assert da.data == db.data and da.packets == db.packets
     assert db.nb_decoded > 0

@@ -2,7 +2,7 @@
 the barrier / max-reduce, both on the box's one GPU) each encode and decode their generation
 shard (netcode_amd.shard.generation_shard id bases) through BatchEncoder / BatchDecoder; the
 union is bit-identical to the oracle over the whole batch.  And bench.py itself under torchrun
-with two ranks (NTC_BENCH_BACKEND=gloo) prints one line with n_gpus = 2 and a verified round
+with two ranks (its default gloo rank sync) prints one line with n_gpus = 2 and a verified round
 trip -- the driver's multi-GPU launch shape, minus RCCL."""
 import json
 import os
@@ -88,7 +88,7 @@ def _ndev():
 
 
 def test_bench_under_torchrun_two_ranks(tmp_path):
-    env = dict(os.environ, NTC_BENCH_BACKEND="gloo")
+    env = {k_: v for k_, v in os.environ.items() if k_ != "NTC_BENCH_BACKEND"}   # the default: gloo
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
@@ -101,4 +101,5 @@ def test_bench_under_torchrun_two_ranks(tmp_path):
     # both ranks share this box's device: the line counts distinct devices and ranks apart
     assert d["ranks"] == 2 and d["n_gpus"] == min(2, _ndev()) and d["value"] > 0
     assert d["verified"]["bit_exact_round_trip"]
+    assert d["rank_sync"] == "gloo"                    # no RCCL for the barrier / max
     assert d["config"]["generations_per_gpu"] == 256

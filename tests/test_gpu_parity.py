@@ -107,6 +107,10 @@ ENCODE_CASES = [
     (600, 16, 4, 1024, 1024, False, "wrap"),          # explicit bases whose products wrap
     # config 2 itself: uint32 wraps make some g / g + 255 matrices differ (those stay unpaired)
     (4096, 32, 8, 1024, 1024, False, "default"),
+    # r > 256: encode_prep walks the coefficients in chunks of 256 rows (two chunks here, the
+    # second ragged); uint32-wrapping ids and unequal lengths (one size product per source)
+    (3, 37, 300, 1024, 1024, True, "wrap"),
+    (2, 64, 513, 512, 512, False, "offset"),
 ]
 
 

@@ -64,6 +64,66 @@ def test_two_rank_sharding_matches_single_process(tmp_path, oracle):
         assert float(z["tmax"][0]) == float(world)
 
 
+def _worker_cfg4(rank, world, port, out_dir, vrank0, vworld, G, k, r, S, pick):
+    """Rank `rank` plays rank vrank0 + rank of a vworld-GPU config-4 run (G generations per GPU),
+    computing the generations `pick` of its shard with the shard's own id bases."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch.distributed as dist
+    from helpers import loss_exact_m, make_sources
+    from netcode_amd.shard import generation_shard, max_over_ranks
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    vr = vrank0 + rank
+    sid, rid = generation_shard(vr, vworld, G, k, r)
+    sid, rid = sid[pick], rid[pick]
+    n = len(pick)
+    src, lens = make_sources(n, k, S, S, seed=100 + vr, ragged=True)
+    rep, rsz = O.encode_batch(src, lens, k, r, sid, rid)
+    mask = loss_exact_m(n, k, r, seed=200 + vr)
+    out, olen, st = O.decode_batch(src * mask[:, :, None], lens * mask, mask, rep, rsz,
+                                   np.ones((n, r), np.uint8), sid, rid)
+    t = max_over_ranks(float(vr), dist)
+    np.savez(os.path.join(out_dir, f"cfg4_{vr}.npz"), sid=sid, rid=rid, rep=rep, rsz=rsz,
+             st=st.view(np.uint8), out=out, olen=olen, tmax=np.array([t]))
+    dist.destroy_process_group()
+
+
+def test_config4_last_ranks_wrapping_ids(tmp_path, oracle):
+    """Config 4 (k=128 r=32, 65536 generations over 8 GPUs): ranks 6 and 7 own the generations
+    whose rid * sid products exceed 2^32 (galois_field.hh:143-158 wraps them).  Two gloo ranks play
+    ranks 6..7; their shard ids equal the single-batch ids of the same generations, and their
+    repairs / decode outcomes equal the oracle's over the whole-batch ids."""
+    import torch.multiprocessing as mp
+    from helpers import loss_exact_m, make_sources
+    from netcode_amd.shard import generation_shard
+    vworld, G, k, r, S = 8, 8192, 128, 32, 64
+    pick = np.array([0, 1, G // 2, G - 2, G - 1])
+    mp.start_processes(_worker_cfg4, args=(2, _free_port(), str(tmp_path), 6, vworld, G, k, r, S, pick),
+                       nprocs=2, join=True, start_method="spawn")
+    sid_all, rid_all = generation_shard(0, 1, G * vworld, k, r)
+    for vr in (6, 7):
+        z = np.load(os.path.join(tmp_path, f"cfg4_{vr}.npz"))
+        g = vr * G + pick
+        assert (z["sid"] == sid_all[g]).all() and (z["rid"] == rid_all[g]).all()
+        # the products of these ids wrap uint32 (the case the shard must not "fix")
+        R1, S1 = rid_all[g].astype(np.uint64) + 1, sid_all[g].astype(np.uint64) + 1
+        assert ((R1 + S1) * R1 > 2**32).all()
+        n = len(pick)
+        src, lens = make_sources(n, k, S, S, seed=100 + vr, ragged=True)
+        rep, rsz = oracle.encode_batch(src, lens, k, r, sid_all[g], rid_all[g])
+        mask = loss_exact_m(n, k, r, seed=200 + vr)
+        out, olen, st = oracle.decode_batch(src * mask[:, :, None], lens * mask, mask, rep, rsz,
+                                            np.ones((n, r), np.uint8), sid_all[g], rid_all[g])
+        assert (z["rep"] == rep).all() and (z["rsz"] == rsz).all()
+        assert (z["st"] == st.view(np.uint8)).all()
+        assert (z["out"] == out).all() and (z["olen"] == olen).all()
+        assert float(z["tmax"][0]) == 7.0
+
+
 def test_shard_ids_wrap_like_uint32():
     from netcode_amd.shard import generation_shard
     sid, rid = generation_shard(7, 8, 8192, 128, 32)

@@ -111,6 +111,8 @@ int main(int argc, char** argv)
   ntc_decoder_t** dec = (ntc_decoder_t**)calloc(F, sizeof(void*));
   ntc_batch_t* eb = batched ? ntc_new_batch() : NULL;
   ntc_batch_t* db = batched ? ntc_new_batch() : NULL;
+  ntc_batch_set_eager(eb, 1);        /* source packets and received deliveries go out at once */
+  ntc_batch_set_eager(db, 1);
   for (uint32_t f = 0; f < F; ++f) {
     ntc_packet_handler h = {&tx[f], on_prepare, on_send};
     enc[f] = ntc_new_encoder(8, h);

@@ -34,7 +34,9 @@ size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT N
  * flush.  Eager mode (ntc_batch_set_eager, off by default) emits an event that needs no GF result
  * (a source packet, a received source's delivery, an ack) of an object with nothing queued at
  * once, inside the call that produced it: callbacks then run both there and at the flush, so a
- * handler must be re-entrant with respect to the objects of the same batch.  Attaching an object
+ * handler must be re-entrant with respect to the objects of the same batch.  Events that handlers
+ * produce during a flush (e.g. a decoder fed from an encoder's packet handler) are queued for the
+ * next flush: flush until ntc_batch_pending is 0 to drain such chains.  Attaching an object
  * to another batch or to NULL flushes its current batch first.
  * Deleting an attached object discards its queued events; deleting a batch discards every queued
  * event and detaches its objects. */

@@ -893,6 +893,101 @@ static void core_free(dec_core* d)
   u32set_free(&d->ordered);
 }
 
+/* ============================================ the streaming decoder as an object (tests) ==== */
+/* detail::decoder (detail/decoder.hh:21-193) over dec_core, for tests/oracle_surface: the reference
+ * Catch suites drive it through their own accessors.  Every call runs in the object's field. */
+struct or_dcore { dec_core core; int w; or_source_fn cb; void* ctx; };
+
+static void dcore_deliver(void* ctx, const dsrc* s)
+{
+  or_dcore* o = (or_dcore*)ctx;
+  if (o->cb) o->cb(o->ctx, s->id, s->data, s->len);
+}
+
+or_dcore* or_dcore_new(int w, int in_order, or_source_fn cb, void* ctx)
+{
+  gf_init();
+  or_dcore* o = calloc(1, sizeof *o);
+  o->w = w; o->cb = cb; o->ctx = ctx;
+  core_init(&o->core, in_order, dcore_deliver, o);
+  return o;
+}
+void or_dcore_free(or_dcore* o) { if (o) { core_free(&o->core); free(o); } }
+
+#define DCORE_FIELD(o, stmt) do { const int old_ = g_w; g_w = (o)->w; stmt; g_w = old_; } while (0)
+
+void or_dcore_add_source(or_dcore* o, uint32_t id, const uint8_t* data, uint16_t len)
+{
+  DCORE_FIELD(o, core_add_source(&o->core, id, data, len));
+}
+void or_dcore_add_repair(or_dcore* o, uint32_t id, const uint32_t* ids, size_t n, uint16_t esz,
+                         const uint8_t* sym, uint16_t symsz)
+{
+  if (n == 0) return;
+  DCORE_FIELD(o, core_add_repair(&o->core, id, ids, n, esz, sym, symsz));
+}
+
+/* decoder.cc:156-178 on a stand-alone one-source repair (bumps nb_decoded).  out receives the
+ * multiply_size(esz, inv) bytes of the source; returns that size. */
+uint16_t or_dcore_create_source_from_repair(or_dcore* o, uint32_t rid, uint32_t sid, uint16_t esz,
+                                            const uint8_t* sym, uint16_t symsz, uint8_t* out)
+{
+  drep r;
+  memset(&r, 0, sizeof r);
+  r.id = rid; r.esz = esz; r.symsz = symsz;
+  r.sym = (uint8_t*)sym;
+  u32set_insert(&r.ids, sid);
+  dsrc s;
+  DCORE_FIELD(o, s = create_source_from_repair(&o->core, &r));
+  u32set_free(&r.ids);
+  memcpy(out, s.data, s.len);
+  free(s.data);
+  return s.len;
+}
+
+/* decoder.cc:182-191 + 393-408 on a stand-alone repair: subtract the source from sym / esz (the
+ * caller drops sid from the repair's id list). */
+void or_dcore_remove_source_from_repair(or_dcore* o, uint32_t sid, const uint8_t* sdata, uint16_t slen,
+                                        uint32_t rid, uint16_t* esz, uint8_t* sym)
+{
+  dsrc s = {sid, slen, (uint8_t*)sdata};
+  drep r;
+  memset(&r, 0, sizeof r);
+  r.id = rid; r.esz = *esz; r.sym = sym;
+  DCORE_FIELD(o, remove_source_data_from_repair(&s, &r));
+  *esz = r.esz;
+}
+
+size_t or_dcore_count(const or_dcore* o, int which)
+{
+  switch (which) {
+    case 0: return o->core.nsrc;
+    case 1: return o->core.nrep;
+    case 2: return o->core.nmiss;
+    case 3: return o->core.nb_decoded;
+    case 4: return o->core.nb_failed;
+    case 5: return o->core.nb_useless;
+    default: return 0;
+  }
+}
+uint32_t or_dcore_source(const or_dcore* o, size_t i, const uint8_t** data, uint16_t* len)
+{
+  *data = o->core.src[i].data; *len = o->core.src[i].len;
+  return o->core.src[i].id;
+}
+uint32_t or_dcore_repair(const or_dcore* o, size_t i, const uint32_t** ids, size_t* n, uint16_t* esz,
+                         const uint8_t** sym, uint16_t* symsz)
+{
+  const drep* r = &o->core.rep[i];
+  *ids = r->ids.v; *n = r->ids.n; *esz = r->esz; *sym = r->sym; *symsz = r->symsz;
+  return r->id;
+}
+uint32_t or_dcore_missing(const or_dcore* o, size_t i, const uint32_t** rids, size_t* n)
+{
+  *rids = o->core.miss[i].rids.v; *n = o->core.miss[i].rids.n;
+  return o->core.miss[i].sid;
+}
+
 /* ===================================================== generation decode (batch form) ====== */
 typedef struct { uint8_t* src; uint32_t stride, sid_base, k; uint16_t* src_len; } gen_sink;
 
@@ -1095,6 +1190,53 @@ size_t or_write_source_packet(uint32_t sid, const uint8_t* data, uint16_t len, u
   return n;
 }
 
+/* packetizer.hh:46-61 write_ack: type 0, packets received since the last ack, source ids. */
+size_t or_write_ack_packet(uint16_t nb_packets, const uint32_t* ids, size_t n, uint8_t* out)
+{
+  bytes b = {0};
+  b_u8(&b, 0); b_u16(&b, nb_packets); write_ids(&b, ids, n);
+  memcpy(out, b.v, b.n);
+  const size_t len = b.n;
+  free(b.v);
+  return len;
+}
+
+size_t or_packet_bound(size_t symsz, size_t nids) { return 15 + 2 * symsz + 4 + 3 * nids; }
+
+/* packet_type.hh get_packet_type (byte 0) + packetizer.hh:64-88 read_ack, :125-163 read_repair,
+ * :186-218 read_source.  Returns the bytes read (the second member of the reference's pair), -1
+ * for a packet of unknown type (packet_type_error), -2 for a truncated one (overflow_error). */
+long or_parse_packet(const uint8_t* pkt, size_t len, or_packet_view* out)
+{
+  memset(out, 0, sizeof *out);
+  if (len == 0) return -1;
+  reader r = {pkt, len, 0};
+  const uint8_t ty = r_u8(&r);
+  if (ty > 2) return -1;
+  out->type = ty;
+  u32set ids = {0};
+  if (ty == 0) {
+    out->nb_packets = r_u16(&r);
+    if (r.err) return -2;
+    read_ids(&r, &ids);
+  } else {
+    out->id = r_u32(&r);
+    out->symbol_size = r_u16(&r);
+    if (r.err || r.left < out->symbol_size) return -2;
+    out->symbol_offset = len - r.left;
+    r.p += out->symbol_size; r.left -= out->symbol_size;
+    if (ty == 1) {
+      read_ids(&r, &ids);
+      out->encoded_size = r_u16(&r);
+    }
+  }
+  if (r.err) { u32set_free(&ids); return -2; }
+  out->ids = ids.v; out->nids = ids.n;
+  return (long)(len - r.left);
+}
+
+void or_packet_view_free(or_packet_view* v) { free(v->ids); v->ids = NULL; v->nids = 0; }
+
 /* One received packet into a batch's generation layout: the device ingestion's specification
    (ntc_gf256_read_packets, include/netcode/gpu.h).  Parsing follows packetizer.hh:125-158
    (read_repair: the first symbol copy, ids, encoded size; overflow_error on truncation) and
@@ -1186,6 +1328,35 @@ size_t or_encoder_nb_sent_repairs(const or_encoder* e) { return e->nb_repairs; }
 size_t or_encoder_nb_sent_sources(const or_encoder* e) { return e->nb_sources; }
 size_t or_encoder_nb_received_acks(const or_encoder* e) { return e->nb_acks; }
 
+/* detail/encoder.cc:15-64 in the calling thread's field: sym[0..max len) = sum_i c(rid, ids[i]) *
+ * syms[i] (each zero-extended), *esz = XOR of the coded lengths.  Returns the symbol length. */
+static uint16_t build_repair(uint32_t rid, size_t n, const uint32_t* ids, const uint8_t* const* syms,
+                             const uint16_t* lens, uint8_t* sym, uint16_t* esz)
+{
+  uint16_t symsz = 0;
+  for (size_t i = 0; i < n; ++i) if (lens[i] > symsz) symsz = lens[i];
+  memset(sym, 0, symsz);
+  uint16_t e = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t c = or_coefficient(rid, ids[i]);
+    if (i == 0) or_region_mul(syms[i], sym, lens[i], c);        /* :26-35 the first source */
+    else or_region_muladd(syms[i], sym, lens[i], c);            /* :38-62 the others */
+    e = (uint16_t)(or_multiply_size(lens[i], c) ^ e);
+  }
+  *esz = e;
+  return symsz;
+}
+
+uint16_t or_build_repair(int w, uint32_t rid, size_t n, const uint32_t* ids, const uint8_t* const* syms,
+                         const uint16_t* lens, uint8_t* sym, uint16_t* esz)
+{
+  gf_init();
+  const int old = g_w; g_w = w;
+  const uint16_t r = build_repair(rid, n, ids, syms, lens, sym, esz);
+  g_w = old;
+  return r;
+}
+
 /* encoder.hh:162-169, 321-333 + packetizer.hh:90-122 */
 static void enc_generate_repair(or_encoder* e)
 {
@@ -1194,13 +1365,11 @@ static void enc_generate_repair(or_encoder* e)
   uint8_t* sym = calloc((size_t)symsz + 16, 1);
   uint16_t esz = 0;
   uint32_t* ids = malloc((e->nwin + 1) * 4);
-  for (size_t i = 0; i < e->nwin; ++i) {
-    const uint32_t c = or_coefficient(e->cur_rid, e->win[i].id);
-    if (i == 0) or_region_mul(e->win[i].data, sym, e->win[i].len, c);
-    else or_region_muladd(e->win[i].data, sym, e->win[i].len, c);
-    esz = (uint16_t)(or_multiply_size(e->win[i].len, c) ^ esz);
-    ids[i] = e->win[i].id;
-  }
+  const uint8_t** syms = malloc((e->nwin + 1) * sizeof(void*));
+  uint16_t* lens = malloc((e->nwin + 1) * 2);
+  for (size_t i = 0; i < e->nwin; ++i) { ids[i] = e->win[i].id; syms[i] = e->win[i].data; lens[i] = e->win[i].len; }
+  build_repair(e->cur_rid, e->nwin, ids, syms, lens, sym, &esz);
+  free(syms); free(lens);
   /* source_ids is a flat_set: ids inserted in window order are ascending */
   bytes b = {0};
   b_u8(&b, 1);
@@ -1253,12 +1422,11 @@ long or_encoder_add_packet(or_encoder* e, const uint8_t* pkt, size_t len)
 {
   if (len == 0 || pkt[0] != 0) return -1;
   e->nb_acks++;
-  reader r = {pkt, len, 0};
-  r_u8(&r);
-  const uint16_t nbp = r_u16(&r);
-  u32set ids;
-  read_ids(&r, &ids);
-  if (r.err) { u32set_free(&ids); return -2; }
+  or_packet_view v;
+  const long consumed = or_parse_packet(pkt, len, &v);
+  if (consumed < 0) return consumed;
+  const uint16_t nbp = v.nb_packets;
+  u32set ids = {v.ids, v.nids, v.nids};
   if (e->adaptive) {
     double loss = 0.0;
     if (e->nb_sent_packets > 0)
@@ -1281,7 +1449,7 @@ long or_encoder_add_packet(or_encoder* e, const uint8_t* pkt, size_t len)
     }
   }
   u32set_free(&ids);
-  return (long)(len - r.left);
+  return consumed;
 }
 
 /* ======================================================== public decoder (decoder.hh) ====== */
@@ -1315,11 +1483,9 @@ void or_decoder_generate_ack(or_decoder* d)
   free(b.v);
 }
 
-/* decoder.hh:231-248, 292-300 */
-static void pub_handle_source(void* ctx, const dsrc* s)
+/* decoder.hh:231-248 */
+void or_decoder_maybe_ack(or_decoder* d)
 {
-  or_decoder* d = (or_decoder*)ctx;
-  d->deliver(d->dctx, s->id, s->data, s->len);
   if (d->ack_packets >= d->ack_nb_packets) {
     or_decoder_generate_ack(d);
     clock_gettime(CLOCK_MONOTONIC, &d->last_ack);
@@ -1331,6 +1497,14 @@ static void pub_handle_source(void* ctx, const dsrc* s)
       d->last_ack = now;
     }
   }
+}
+
+/* decoder.hh:292-300 */
+static void pub_handle_source(void* ctx, const dsrc* s)
+{
+  or_decoder* d = (or_decoder*)ctx;
+  d->deliver(d->dctx, s->id, s->data, s->len);
+  or_decoder_maybe_ack(d);
 }
 
 or_decoder* or_decoder_new(int in_order, or_emit_fn emit, void* ectx, or_deliver_fn deliver,
@@ -1368,36 +1542,21 @@ size_t or_decoder_counter(const or_decoder* d, int which)
 /* decoder.hh:88-122 + packetizer.hh:125-218 */
 static long dec_add_packet(or_decoder* d, const uint8_t* pkt, size_t len)
 {
-  if (len == 0) return -1;
-  reader r = {pkt, len, 0};
-  const uint8_t ty = r_u8(&r);
-  if (ty == 1) {
-    d->nb_rrep++;
-    d->ack_packets++;
-    const uint32_t id = r_u32(&r);
-    const uint16_t symsz = r_u16(&r);
-    if (r.err || r.left < symsz) return -2;
-    const uint8_t* sym = r.p;
-    r.p += symsz; r.left -= symsz;
-    u32set ids;
-    read_ids(&r, &ids);
-    const uint16_t esz = r_u16(&r);
-    if (r.err) { u32set_free(&ids); return -2; }
-    const long consumed = (long)(len - r.left);
-    if (ids.n) core_add_repair(&d->core, id, ids.v, ids.n, esz, sym, symsz);
-    u32set_free(&ids);
-    return consumed;
-  } else if (ty == 2) {
-    d->nb_rsrc++;
-    d->ack_packets++;
-    const uint32_t id = r_u32(&r);
-    const uint16_t sz = r_u16(&r);
-    if (r.err || r.left < sz) return -2;
-    const long consumed = (long)(len - r.left + sz);
-    core_add_source(&d->core, id, r.p, sz);
-    return consumed;
+  if (len == 0 || (pkt[0] != 1 && pkt[0] != 2)) return -1;     /* decoder.hh:117-120 */
+  if (pkt[0] == 1) d->nb_rrep++;                                 /* counted before parsing */
+  else d->nb_rsrc++;
+  d->ack_packets++;
+  or_packet_view v;
+  const long consumed = or_parse_packet(pkt, len, &v);
+  if (consumed < 0) return consumed;
+  if (v.type == 1) {
+    if (v.nids) core_add_repair(&d->core, v.id, v.ids, v.nids, v.encoded_size, pkt + v.symbol_offset,
+                                v.symbol_size);
+  } else {
+    core_add_source(&d->core, v.id, pkt + v.symbol_offset, v.symbol_size);
   }
-  return -1;
+  or_packet_view_free(&v);
+  return consumed;
 }
 
 /* ============================================================= loss models =============== */

@@ -168,6 +168,48 @@ int or_read_packet_into(const uint8_t* pkt, size_t len, uint32_t G, uint32_t k, 
                         uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
                         uint8_t* rep_mask);
 
+/* --------------------------------------- packet-level pieces for tests/oracle_surface ------ */
+/* The reference's detail layer over this restatement (tests only): the reference's own Catch suites
+ * and end_to_end.cc compile against the headers under tests/oracle_surface/ and run HERE, so the checker is
+ * pinned by the reference's own expectations. */
+typedef struct {
+  uint8_t  type;            /* 0 ack, 1 repair, 2 source */
+  uint32_t id;              /* repair / source id */
+  uint16_t nb_packets;      /* ack */
+  uint16_t encoded_size;    /* repair */
+  uint16_t symbol_size;     /* repair / source */
+  size_t   symbol_offset;   /* the (first) symbol copy, from the packet start */
+  uint32_t* ids; size_t nids;   /* ack / repair: sorted unique source ids (malloc'd) */
+} or_packet_view;
+long   or_parse_packet(const uint8_t* pkt, size_t len, or_packet_view* out);  /* -1 type, -2 overflow */
+void   or_packet_view_free(or_packet_view*);
+size_t or_write_ack_packet(uint16_t nb_packets, const uint32_t* ids, size_t n, uint8_t* out);
+size_t or_packet_bound(size_t symsz, size_t nids);     /* bytes a repair / ack packet may need */
+/* detail/encoder.cc:15-64 in field w: returns the repair symbol length (max of lens). */
+uint16_t or_build_repair(int w, uint32_t rid, size_t n, const uint32_t* ids, const uint8_t* const* syms,
+                         const uint16_t* lens, uint8_t* sym, uint16_t* esz);
+void   or_decoder_maybe_ack(or_decoder*);           /* decoder.hh:231-248 */
+
+/* detail::decoder (detail/decoder.hh) as an object: the streaming core the public decoder and
+ * or_decode_batch run. */
+typedef struct or_dcore or_dcore;
+typedef void (*or_source_fn)(void* ctx, uint32_t id, const uint8_t* bytes, uint16_t len);
+or_dcore* or_dcore_new(int w, int in_order, or_source_fn cb, void* ctx);
+void      or_dcore_free(or_dcore*);
+void      or_dcore_add_source(or_dcore*, uint32_t id, const uint8_t* data, uint16_t len);
+void      or_dcore_add_repair(or_dcore*, uint32_t id, const uint32_t* ids, size_t n, uint16_t esz,
+                              const uint8_t* sym, uint16_t symsz);
+uint16_t  or_dcore_create_source_from_repair(or_dcore*, uint32_t rid, uint32_t sid, uint16_t esz,
+                                             const uint8_t* sym, uint16_t symsz, uint8_t* out);
+void      or_dcore_remove_source_from_repair(or_dcore*, uint32_t sid, const uint8_t* sdata,
+                                             uint16_t slen, uint32_t rid, uint16_t* esz, uint8_t* sym);
+/* which: 0 sources, 1 repairs, 2 missing sources, 3 nb_decoded, 4 nb_failed, 5 nb_useless */
+size_t    or_dcore_count(const or_dcore*, int which);
+uint32_t  or_dcore_source(const or_dcore*, size_t i, const uint8_t** data, uint16_t* len);
+uint32_t  or_dcore_repair(const or_dcore*, size_t i, const uint32_t** ids, size_t* n, uint16_t* esz,
+                          const uint8_t** sym, uint16_t* symsz);
+uint32_t  or_dcore_missing(const or_dcore*, size_t i, const uint32_t** rids, size_t* n);
+
 /* bench.py --per-packet CPU leg (C level): see ntc_oracle.c.  secs[2], counts[4], hashes[2]. */
 int or_pp_bench(uint32_t flows, uint32_t items, uint32_t size, uint32_t window, uint32_t rate,
                 uint32_t loss_pct, uint64_t seed, double* secs, uint64_t* counts, uint64_t* hashes);

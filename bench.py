@@ -596,6 +596,61 @@ def per_packet_main(a):
         sys.exit(3)
 
 
+def host_rate_wire(w, reps=3):
+    """Host-resident rate through the WIRE format (PCIe-inclusive GiB/s of source payload, never
+    `value`), socket buffer to socket buffer: sender = sources H2D -> encode -> write_repairs ->
+    repair packets D2H; receiver = its received source packets + the repair packets H2D ->
+    read_packets (+ _append) -> decode -> pack_slots of the lost rows -> D2H
+    (HostPipeline.encode_decode_wire, chunks of G/16 over 3 streams).  Returns (GiB/s, ok, repair
+    packets of the run [G*r, rps] host, lengths): ok = the repair packets equal the device-resident
+    Wire.write_repairs of the same repairs, and every decoded generation's recovered rows and sizes
+    equal its lost sources."""
+    from netcode_amd.engine import Wire
+    from netcode_amd.pipeline import HostPipeline
+    dev, G, k, r, stride = w.dev, w.G, w.k, w.r, w.stride
+    wire = Wire(dev)
+    pin = lambda t: torch.empty_like(t, device="cpu").pin_memory().copy_(t)
+    # the receiver's socket buffers: the source packets that were not lost, generation-major
+    spk, slen = wire.write_sources(w.src, w.src_len, w.sid)
+    keep = (w.smask.reshape(-1) != 0).nonzero().reshape(-1)
+    h_rxp, h_rxl = pin(spk.index_select(0, keep)), pin(slen.index_select(0, keep))
+    cnt = (w.smask != 0).sum(1).cpu().to(torch.int64)
+    rx_first = torch.zeros(G + 1, dtype=torch.int64)
+    rx_first[1:] = torch.cumsum(cnt, 0)
+    rpk_dev, rlen_dev = wire.write_repairs(w.out, k, w.sid, w.rid)
+    rps = rpk_dev.shape[1]
+    h_src, h_len, h_mask = pin(w.src), pin(w.src_len), pin(w.smask)
+    h_rep_pkts = torch.empty((G * r, rps), dtype=torch.uint8).pin_memory()
+    h_rep_len = torch.empty((G * r,), dtype=torch.int32).pin_memory()
+    _, _, _, n_lost = HostPipeline.row_bases(h_mask)
+    h_rec = torch.empty((n_lost, stride), dtype=torch.uint8).pin_memory()
+    h_dec_len = torch.empty((G, k), dtype=torch.int16).pin_memory()
+    h_st = torch.empty((G, 12), dtype=torch.uint8).pin_memory()
+    sid_h = w.sid.cpu().numpy().view(np.uint32)
+    rid_h = w.rid.cpu().numpy().view(np.uint32)
+    pipe = HostPipeline(k, r, stride, max(1, G // 16), dev, depth=3)
+    torch.cuda.synchronize(dev)
+    times = []
+    for _ in range(reps + 1):                  # the first pass warms the streams / engines
+        t0 = time.perf_counter()
+        pipe.encode_decode_wire(h_src, h_len, h_rep_pkts, h_rep_len, h_rxp, h_rxl, rx_first, h_mask,
+                                h_rec, h_dec_len, h_st, sid_h, rid_h, w.sid, w.rid)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    rate = G * k * w.S / min(times[1:]) / 2**30
+    ok = torch.equal(h_rep_pkts, rpk_dev.cpu()) and torch.equal(h_rep_len, rlen_dev.cpu())
+    from netcode_amd import status_to_numpy
+    st = status_to_numpy(h_st)
+    lost = (w.smask == 0).cpu()
+    dec = torch.from_numpy(st["state"] == 0)
+    rec_gen = torch.repeat_interleave(torch.arange(G), lost.sum(1))   # generation of each lost row
+    src_lost = w.src.cpu()[lost]
+    sel = dec[rec_gen]
+    ok = ok and torch.equal(h_rec[sel], src_lost[sel])
+    ok = ok and torch.equal(h_dec_len[lost][sel], w.src_len.cpu()[lost][sel])
+    return rate, bool(ok), h_rep_pkts, h_rep_len
+
+
 def oracle_check(smp, threads):
     """cpu_baseline leg (the oracle is the checker here, never the measured path): the sampled
     generations of the bench's own last step against the oracle on the same sources, lengths, id
@@ -608,6 +663,18 @@ def oracle_check(smp, threads):
     lost = smp["src"] * smp["mask"][:, :, None]
     out, olen, ost = O.decode_batch(lost, smp["len"] * smp["mask"], smp["mask"], orep, orsz,
                                     smp["rmask"], smp["sid"], smp["rid"], threads=threads)
+    # the wire leg's repair packets of these generations against the oracle's packetizer
+    # (packetizer.hh:90-122) over the oracle's own repairs
+    pk_ok = None
+    if smp.get("rep_pkts") is not None:
+        pk_ok = True
+        for gi in range(len(smp["g"])):
+            ids = (smp["sid"][gi].astype(np.uint64) + np.arange(k, dtype=np.uint64)) & 0xFFFFFFFF
+            L = int(smp["len"][gi].max())
+            for j in range(r):
+                ref = O.write_repair_packet(int(smp["rid"][gi]) + j, orep[gi, j, :L], ids, int(orsz[gi, j]))
+                got = smp["rep_pkts"][gi, j, :int(smp["rep_pkt_len"][gi, j])].tobytes()
+                pk_ok = pk_ok and ref == got
     # slots the decoder owns: every slot of a decoded generation, the received ones otherwise (the
     # lost slots of a generation that does not decode are not written by either side)
     own = (ost["state"] == 0)[:, None] | (smp["mask"] != 0)
@@ -615,6 +682,7 @@ def oracle_check(smp, threads):
            "status": bool((ost == smp["status"]).all()),
            "decoded_slots": bool((out[own] == smp["rx"][own]).all()),
            "decoded_lengths": bool((olen == smp["rx_len"]).all()),
+           **({"wire_repair_packets": pk_ok} if pk_ok is not None else {}),
            "decoded_generations": int((ost["state"] == 0).sum()),
            "singular_generations": int((ost["state"] == 3).sum())}
     return all(v for k_, v in res.items() if isinstance(v, bool)), res
@@ -890,8 +958,22 @@ def main():
                                       "then only the received sources H2D and only the lost "
                                       "slots D2H (packed rows), 3 streams")
         line["host_resident_bit_exact"] = hok
+        good = good and hok
         line["host_resident_full_slots_GiBps"] = round(hp, 3)
         line["host_resident_serial_GiBps"] = round(hs, 3)
+        hw, hwok, rpk, rpl = host_rate_wire(w)
+        line["host_resident_wire_GiBps"] = round(hw, 3)
+        line["host_resident_wire_note"] = (
+            "PCIe-inclusive, never `value`, socket buffer to socket buffer in the reference's wire "
+            "format: sender sources H2D -> encode -> write_repairs -> repair packets D2H; receiver "
+            "received source packets + repair packets H2D -> read_packets -> decode -> lost rows "
+            "packed D2H; 3 streams, chunks of G/16")
+        line["host_resident_wire_bit_exact"] = hwok
+        good = good and hwok
+        if smp is not None:
+            gi = torch.from_numpy(smp["g"])
+            smp["rep_pkts"] = rpk.view(G, r, -1)[gi].numpy()
+            smp["rep_pkt_len"] = rpl.view(G, r)[gi].numpy()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         _, _, usable = cpu_info()
         thr = a.cpu_threads or usable          # every CPU this process may run on

@@ -246,6 +246,14 @@ int  ntc_gf256_read_packets(ntc_gf256_engine* eng, uint32_t npkts, const uint8_t
                             uint32_t r, uint32_t stride, uint32_t sid0, uint32_t rid0,
                             uint8_t* src, uint16_t* src_len, uint8_t* src_mask, uint8_t* rep,
                             uint16_t* rep_size, uint8_t* rep_mask, uint8_t* status, void* stream);
+/* The same without the reset: the packets of a further recvmmsg batch (e.g. another packet size's
+ * slots) are added to what earlier read_packets / read_packets_append calls stored. */
+int  ntc_gf256_read_packets_append(ntc_gf256_engine* eng, uint32_t npkts, const uint8_t* pkts,
+                                   uint32_t pkt_stride, const uint32_t* pkt_len, uint32_t G,
+                                   uint32_t k, uint32_t r, uint32_t stride, uint32_t sid0,
+                                   uint32_t rid0, uint8_t* src, uint16_t* src_len, uint8_t* src_mask,
+                                   uint8_t* rep, uint16_t* rep_size, uint8_t* rep_mask,
+                                   uint8_t* status, void* stream);
 
 /* ---- Packed rows <-> generation slots (host-resident batches) ---------------------------------
  * A receiver holds only the sources it received and wants back only the ones it lost; these two

@@ -22,7 +22,7 @@ GPU_H_SYMBOLS = [
     "ntc_gf256_last_error", "ntc_gf256_build_info",
     "ntc_gf256_dense_invert_batch", "ntc_gf256_dense_encode_batch", "ntc_gf256_dense_decode_batch",
     "ntc_gf256_repair_packet_bytes", "ntc_gf256_write_repairs", "ntc_gf256_write_sources",
-    "ntc_gf256_read_packets", "ntc_gf256_unpack_slots", "ntc_gf256_pack_slots",
+    "ntc_gf256_read_packets", "ntc_gf256_read_packets_append", "ntc_gf256_unpack_slots", "ntc_gf256_pack_slots",
     "ntc_gf_combine_batch", "ntc_gf_region_multiply", "ntc_gf_coefficient", "ntc_gf_multiply",
     "ntc_gf_invert", "ntc_gf_multiply_size", "ntc_gf256_set_timing", "ntc_gf256_mac_time",
     "ntc_gf256_set_plan_kind", "ntc_gf256_timing_log", "ntc_gf256_timing_read", "ntc_gf256_timing_kinds",
@@ -91,6 +91,7 @@ def load(path: str | None = None):
     L.ntc_gf256_write_sources.argtypes = [V, u32, u32, u32, P, P, P, P, u32, P, V]
     L.ntc_gf256_read_packets.argtypes = [V, u32, P, u32, P, u32, u32, u32, u32, u32, u32,
                                          P, P, P, P, P, P, P, V]
+    L.ntc_gf256_read_packets_append.argtypes = L.ntc_gf256_read_packets.argtypes
     L.ntc_gf256_unpack_slots.argtypes = [V, u32, u32, u32, P, P, u32, P, u8, P, C.c_int, V]
     L.ntc_gf256_pack_slots.argtypes = [V, u32, u32, u32, P, P, u8, P, u32, P, V]
     L.ntc_gf256_set_timing.argtypes = [V, C.c_int]

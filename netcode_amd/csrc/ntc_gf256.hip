@@ -473,7 +473,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   static_assert(R == 8 || R == 16, "8- or 16-row tiles");
   static_assert(!PAIR || (!DEC && !FULL), "pairing is an encode mode for short symbols");
   static_assert(kBsRing == 4, "the unrolled loop assumes a 4-slot ring");
-  constexpr bool kLate = R == 16;
+  constexpr bool kLate = R == 16 && !FULL;
   using CoefV = typename BsCoef<R>::T;
   const size_t stride = a.stride;
   const uint32_t k = i_count ? i_count : a.k;           // sources this wave sums (split-k: a part)
@@ -1693,9 +1693,21 @@ __device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], uint32_t m, const 
   }
 }
 
+#ifdef NTC_PLAN_CLOCK
+__device__ uint64_t g_dbg_clk[1 << 18];
+extern "C" int ntc_dbg_plan_clock(uint64_t* out, uint32_t n)
+{
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_clk), n * 8) == hipSuccess ? 0 : -1;
+}
+#define DBG_CLK(slot) uint64_t dbg_t##slot = wall_clock64()
+#else
+#define DBG_CLK(slot)
+#endif
+
 template <int RM>
 __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 {
+  DBG_CLK(0);
   static_assert(RM == 8 || RM == 16 || RM == 32, "the column layout needs 2 * RM <= 64 lanes");
   constexpr int W = RM / 4;
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
@@ -1868,6 +1880,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
     uint32_t col[W];
     bool ok = false;
     uint32_t t = m - 1;
+    DBG_CLK(1);
     for (; t < nrecv; ++t) {
       // row m-1: received repair t (decoder.cc:448-468 retries with each newer repair)
       const uint32_t ct = coef(__builtin_amdgcn_readlane(rid1, t));
@@ -1877,6 +1890,10 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       if (gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
       if (t == m - 1 && t + 1 < nrecv) t = screen_candidates() - 1;   // the loop's ++t: next
     }
+#ifdef NTC_PLAN_CLOCK
+    uint64_t dbg_t2 = wall_clock64();
+    if (lane == 0) { g_dbg_clk[8 * g + 1] = dbg_t1; g_dbg_clk[8 * g + 2] = dbg_t2; }
+#endif
     if (!ok) {
       st.state = 3;
       const uint32_t f = nrecv - m + 1;
@@ -2029,6 +2046,17 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   if (lane == 0) {
     a.plan_m[g] = static_cast<uint16_t>(mm);
     a.status[g] = st;
+#ifdef NTC_PLAN_CLOCK
+    g_dbg_clk[8 * g + 0] = dbg_t0;
+    g_dbg_clk[8 * g + 3] = wall_clock64();
+    g_dbg_clk[8 * g + 4] = st.state;
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_dbg_clk[8 * g + 5] = hw;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_dbg_clk[8 * g + 6] = xcc;
+#endif
   }
 }
 

@@ -435,11 +435,11 @@ int ntc_gf256_write_sources(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_
   return hip_check(hipGetLastError(), "wire_write_sources launch");
 }
 
-int ntc_gf256_read_packets(ntc_gf256_engine* e, uint32_t npkts, const uint8_t* pkts,
-                           uint32_t pkt_stride, const uint32_t* pkt_len, uint32_t G, uint32_t k,
-                           uint32_t r, uint32_t stride, uint32_t sid0, uint32_t rid0, uint8_t* src,
-                           uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
-                           uint8_t* rep_mask, uint8_t* status, void* stream)
+static int read_packets_impl(bool reset, ntc_gf256_engine* e, uint32_t npkts, const uint8_t* pkts,
+                             uint32_t pkt_stride, const uint32_t* pkt_len, uint32_t G, uint32_t k,
+                             uint32_t r, uint32_t stride, uint32_t sid0, uint32_t rid0, uint8_t* src,
+                             uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
+                             uint8_t* rep_mask, uint8_t* status, void* stream)
 {
   if (!e || !src || !src_len || !src_mask || !rep || !rep_size || !rep_mask)
     return fail(NTC_GPU_EINVAL, "NULL argument");
@@ -452,15 +452,37 @@ int ntc_gf256_read_packets(ntc_gf256_engine* e, uint32_t npkts, const uint8_t* p
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t nk = static_cast<size_t>(G) * k, nr = static_cast<size_t>(G) * r;
   int rc;
-  if ((rc = hip_check(hipMemsetAsync(src_mask, 0, nk, st), "reset src_mask"))) return rc;
-  if ((rc = hip_check(hipMemsetAsync(src_len, 0, 2 * nk, st), "reset src_len"))) return rc;
-  if ((rc = hip_check(hipMemsetAsync(rep_mask, 0, nr, st), "reset rep_mask"))) return rc;
-  if ((rc = hip_check(hipMemsetAsync(rep_size, 0, 2 * nr, st), "reset rep_size"))) return rc;
+  if (reset) {
+    if ((rc = hip_check(hipMemsetAsync(src_mask, 0, nk, st), "reset src_mask"))) return rc;
+    if ((rc = hip_check(hipMemsetAsync(src_len, 0, 2 * nk, st), "reset src_len"))) return rc;
+    if ((rc = hip_check(hipMemsetAsync(rep_mask, 0, nr, st), "reset rep_mask"))) return rc;
+    if ((rc = hip_check(hipMemsetAsync(rep_size, 0, 2 * nr, st), "reset rep_size"))) return rc;
+  }
   if (npkts == 0) return NTC_GPU_OK;
   ReadArgs a{npkts, pkt_stride, pkts, pkt_len, G, k, r, stride, sid0, rid0,
              src, src_len, src_mask, rep, rep_size, rep_mask, status};
   hipLaunchKernelGGL(wire_read_packets, dim3(npkts), dim3(kWireThreads), 0, st, a);
   return hip_check(hipGetLastError(), "wire_read_packets launch");
+}
+
+int ntc_gf256_read_packets(ntc_gf256_engine* e, uint32_t npkts, const uint8_t* pkts,
+                           uint32_t pkt_stride, const uint32_t* pkt_len, uint32_t G, uint32_t k,
+                           uint32_t r, uint32_t stride, uint32_t sid0, uint32_t rid0, uint8_t* src,
+                           uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
+                           uint8_t* rep_mask, uint8_t* status, void* stream)
+{
+  return read_packets_impl(true, e, npkts, pkts, pkt_stride, pkt_len, G, k, r, stride, sid0, rid0, src,
+                           src_len, src_mask, rep, rep_size, rep_mask, status, stream);
+}
+
+int ntc_gf256_read_packets_append(ntc_gf256_engine* e, uint32_t npkts, const uint8_t* pkts,
+                                  uint32_t pkt_stride, const uint32_t* pkt_len, uint32_t G, uint32_t k,
+                                  uint32_t r, uint32_t stride, uint32_t sid0, uint32_t rid0, uint8_t* src,
+                                  uint16_t* src_len, uint8_t* src_mask, uint8_t* rep, uint16_t* rep_size,
+                                  uint8_t* rep_mask, uint8_t* status, void* stream)
+{
+  return read_packets_impl(false, e, npkts, pkts, pkt_stride, pkt_len, G, k, r, stride, sid0, rid0, src,
+                           src_len, src_mask, rep, rep_size, rep_mask, status, stream);
 }
 
 int ntc_gf256_unpack_slots(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t stride,

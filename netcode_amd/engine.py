@@ -390,7 +390,9 @@ class Wire:
 
     def read_packets(self, pkts: torch.Tensor, pkt_len: torch.Tensor, G: int, k: int, r: int,
                      stride: int, sid0: int = 0, rid0: int = 0,
-                     out: ReceivedBatch | None = None) -> ReceivedBatch:
+                     out: ReceivedBatch | None = None, append: bool = False) -> ReceivedBatch:
+        """append=True (ntc_gf256_read_packets_append): add to `out` what earlier calls stored
+        instead of resetting its lengths / masks first (a second recvmmsg batch)."""
         n, pkt_stride = pkts.shape
         dev = self.device
         _require(pkts, "pkts", _U8, (n, pkt_stride), dev)
@@ -404,7 +406,13 @@ class Wire:
                 torch.empty((G, r), dtype=torch.int16, device=dev),
                 torch.empty((G, r), dtype=torch.uint8, device=dev),
                 torch.empty((n,), dtype=torch.uint8, device=dev))
-        _native.check(_native.load().ntc_gf256_read_packets(
+        if append and out is None:
+            raise ValueError("append needs the batch of an earlier read_packets call")
+        if out is not None and out.status.numel() < n:
+            raise ValueError(f"out.status holds {out.status.numel()} packet outcomes, {n} packets given")
+        L = _native.load()
+        fn = L.ntc_gf256_read_packets_append if append else L.ntc_gf256_read_packets
+        _native.check(fn(
             self.engine.handle, n, pkts.data_ptr(), pkt_stride, pkt_len.data_ptr(), G, k, r,
             stride, sid0 & 0xFFFFFFFF, rid0 & 0xFFFFFFFF, out.src.data_ptr(),
             out.src_len.data_ptr(), out.src_mask.data_ptr(), out.rep.data_ptr(),

@@ -239,6 +239,102 @@ class HostPipeline:
                 h_status[g0:g1].copy_(st, non_blocking=True)
         self._join()
 
+    def encode_decode_wire(self, h_src, h_src_len, h_rep_pkts, h_rep_pkt_len, h_rx_pkts, h_rx_pkt_len,
+                           rx_first, h_mask, h_rec_packed, h_dec_len, h_status, sid_host, rid_host,
+                           sid_base, rid_base):
+        """Loopback of one batch through the WIRE format, socket buffer to socket buffer (the path of
+        the reference's examples: the sender hands payloads in and takes packets out; the receiver
+        hands packets in and takes recovered payloads out).  Per chunk of generations:
+
+        * sender: sources H2D -> encode -> ``write_repairs`` (packetizer.hh:90-122) -> the repair
+          packets D2H into h_rep_pkts [G*r, rps] / h_rep_pkt_len [G*r] (a sendmmsg batch; the source
+          packets are the caller's payloads behind a 7-byte header);
+        * receiver: its received packets H2D -- the source packets h_rx_pkts [N, sps] /
+          h_rx_pkt_len [N] (generations g0..g1 own rows rx_first[g0]..rx_first[g1]) and the repair
+          packets the sender put in h_rep_pkts -- -> ``read_packets`` + ``read_packets_append``
+          (decoder.hh dispatch + read_source / read_repair) into its own slots -> decode -> the
+          LOST slots packed (``pack_slots``) and D2H into h_rec_packed [n_lost, stride], the
+          decoded sizes into h_dec_len [G, k], the status into h_status.
+
+        sid_host / rid_host: the u32 id bases as host sequences (read_packets maps ids to slots
+        from the chunk's first bases); sid_base / rid_base the same on the device.  The lost rows'
+        offsets come from h_mask, the loss pattern the caller applied."""
+        from .engine import ReceivedBatch, Wire
+        G = h_src.shape[0]
+        k, r, stride = self.k, self.r, self.stride
+        self._check(G, h_src=h_src, h_src_len=h_src_len, h_mask=h_mask, h_status=h_status)
+        self._check_bases(G, sid_base=sid_base, rid_base=rid_base)
+        rps = Wire.repair_packet_bytes(k, stride)
+        for name, t, shape, dt in (("h_rep_pkts", h_rep_pkts, (G * r, rps), torch.uint8),
+                                   ("h_rep_pkt_len", h_rep_pkt_len, (G * r,), torch.int32),
+                                   ("h_rx_pkt_len", h_rx_pkt_len, (h_rx_pkts.shape[0],), torch.int32),
+                                   ("h_dec_len", h_dec_len, (G, k), torch.int16)):
+            _pinned(t, name)
+            if t.dtype != dt or tuple(t.shape) != shape:
+                raise ValueError(f"{name} must be {dt} {shape}, got {t.dtype} {tuple(t.shape)}")
+        _pinned(h_rx_pkts, "h_rx_pkts")
+        sps = h_rx_pkts.shape[1]
+        _, lost_base, _, n_lost = self.row_bases(h_mask)
+        wire = Wire(self.device)
+        dev = self.device
+        if not hasattr(self, "d_rows"):
+            self.d_rows = [torch.empty((self.chunk * k, stride), dtype=torch.uint8, device=dev)
+                           for _ in range(self.depth)]
+        if getattr(self, "_wire_cap", None) != (rps, sps):
+            C, D = self.chunk, self.depth
+            self.d_rep_pkts = [torch.empty((C * r, rps), dtype=torch.uint8, device=dev) for _ in range(D)]
+            self.d_rep_pkt_len = [torch.empty((C * r,), dtype=torch.int32, device=dev) for _ in range(D)]
+            self.d_rx_rep_pkts = [torch.empty((C * r, rps), dtype=torch.uint8, device=dev) for _ in range(D)]
+            self.d_rx_rep_len = [torch.empty((C * r,), dtype=torch.int32, device=dev) for _ in range(D)]
+            self.d_rx_pkts = [torch.empty((C * k, sps), dtype=torch.uint8, device=dev) for _ in range(D)]
+            self.d_rx_pkt_len = [torch.empty((C * k,), dtype=torch.int32, device=dev) for _ in range(D)]
+            self.d_pkt_status = [torch.empty((C * (k + r),), dtype=torch.uint8, device=dev) for _ in range(D)]
+            # the receiver's own slots: nothing of the sender's buffers is visible to it
+            self.d_rxs = [torch.empty((C, k, stride), dtype=torch.uint8, device=dev) for _ in range(D)]
+            self.d_rxrep = [torch.empty((C, r, stride), dtype=torch.uint8, device=dev) for _ in range(D)]
+            self.d_rxrsz = [torch.empty((C, r), dtype=torch.int16, device=dev) for _ in range(D)]
+            self._wire_cap = (rps, sps)
+        d_lost_base = lost_base.to(dev)
+        self._fork()
+        for s, g0, g1 in self._chunks(G):
+            n = g1 - g0
+            p0, p1 = int(rx_first[g0]), int(rx_first[g1])
+            l0, l1 = int(lost_base[g0]), (int(lost_base[g1]) if g1 < G else n_lost)
+            with torch.cuda.stream(self.streams[s]):
+                buf, ln, mk, rmk = self.d_src[s][:n], self.d_len[s][:n], self.d_mask[s][:n], self.d_rmask[s][:n]
+                out, st, rows = self.d_out[s], self.d_status[s][:n], self.d_rows[s]
+                o = EncodeResult(out.repairs[:n], out.encoded_size[:n], out.symbol_len[:n])
+                sid, rid = sid_base[g0:g1], rid_base[g0:g1]
+                # sender
+                buf.copy_(h_src[g0:g1], non_blocking=True)
+                ln.copy_(h_src_len[g0:g1], non_blocking=True)
+                self.enc[s](buf, ln, sid, rid, o)
+                rp, rl = self.d_rep_pkts[s][:n * r], self.d_rep_pkt_len[s][:n * r]
+                _native_write_repairs(wire, o, k, sid, rid, rp, rl)
+                h_rep_pkts[g0 * r:g1 * r].copy_(rp, non_blocking=True)
+                h_rep_pkt_len[g0 * r:g1 * r].copy_(rl, non_blocking=True)
+                # receiver: source packets, then the repair packets back from the sender's host
+                # buffer (stream order: after their D2H), into slots of its own
+                xp, xl = self.d_rx_pkts[s][:p1 - p0], self.d_rx_pkt_len[s][:p1 - p0]
+                xp.copy_(h_rx_pkts[p0:p1], non_blocking=True)
+                xl.copy_(h_rx_pkt_len[p0:p1], non_blocking=True)
+                yp, yl = self.d_rx_rep_pkts[s][:n * r], self.d_rx_rep_len[s][:n * r]
+                yp.copy_(h_rep_pkts[g0 * r:g1 * r], non_blocking=True)
+                yl.copy_(h_rep_pkt_len[g0 * r:g1 * r], non_blocking=True)
+                rx, rrep, rrsz = self.d_rxs[s][:n], self.d_rxrep[s][:n], self.d_rxrsz[s][:n]
+                rb = ReceivedBatch(rx, ln, mk, rrep, rrsz, rmk, self.d_pkt_status[s][:p1 - p0])
+                wire.read_packets(xp, xl, n, k, r, stride, int(sid_host[g0]), int(rid_host[g0]), out=rb)
+                rb.status = self.d_pkt_status[s][p1 - p0:p1 - p0 + n * r]
+                wire.read_packets(yp, yl, n, k, r, stride, int(sid_host[g0]), int(rid_host[g0]), out=rb,
+                                  append=True)
+                self.dec[s](rx, ln, mk, rrep, rrsz, rmk, sid, rid, st)
+                if l1 > l0:
+                    wire.pack_slots(rx, mk, d_lost_base[g0:g1], rows[:l1 - l0], want=0, row0=l0)
+                    h_rec_packed[l0:l1].copy_(rows[:l1 - l0], non_blocking=True)
+                h_dec_len[g0:g1].copy_(ln, non_blocking=True)
+                h_status[g0:g1].copy_(st, non_blocking=True)
+        self._join()
+
     def encode_decode(self, h_src, h_src_len, h_rep, h_rep_size, h_rx, h_rx_len, h_mask, h_rmask,
                       h_status, sid_base=None, rid_base=None):
         """Loopback of one batch (bench.py's host-resident rate): per chunk, sources H2D -> encode
@@ -270,3 +366,14 @@ class HostPipeline:
                 h_rx_len[g0:g1].copy_(ln, non_blocking=True)
                 h_status[g0:g1].copy_(st, non_blocking=True)
         self._join()
+
+
+def _native_write_repairs(wire, enc, k, sid, rid, pkts, lens):
+    """ntc_gf256_write_repairs into caller-owned packet slots (Wire.write_repairs allocates)."""
+    from . import _native
+    from .engine import _ptr, _stream
+    G, r, stride = enc.repairs.shape
+    _native.check(_native.load().ntc_gf256_write_repairs(
+        wire.engine.handle, G, k, r, stride, enc.repairs.data_ptr(), enc.encoded_size.data_ptr(),
+        enc.symbol_len.data_ptr(), _ptr(sid), _ptr(rid), pkts.data_ptr(), pkts.shape[1],
+        lens.data_ptr(), _stream(wire.device)), "ntc_gf256_write_repairs")

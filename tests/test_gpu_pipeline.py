@@ -174,3 +174,66 @@ def test_pipeline_rejects_pageable(gpu):
         p.encode(src, torch.zeros((3, 4), dtype=torch.int16).pin_memory(),
                  torch.zeros((3, 2, 64), dtype=torch.uint8).pin_memory(),
                  torch.zeros((3, 2), dtype=torch.int16).pin_memory())
+
+
+@pytest.mark.parametrize("G,chunk,depth,S", [(21, 8, 3, 1024), (6, 6, 2, 1500)])
+def test_wire_pipeline_matches_oracle(gpu, G, chunk, depth, S):
+    """HostPipeline.encode_decode_wire (socket buffer to socket buffer in the reference's wire
+    format): the sender's repair packets equal the oracle's packetizer (packetizer.hh:90-122) over
+    the oracle's repairs; the receiver, fed the received source packets (oracle packetizer,
+    packetizer.hh:165-183) and the sender's repair packets, returns the oracle's status, recovered
+    rows and decoded sizes.  Continuous ids that wrap u32 between generations."""
+    import torch
+    from netcode_amd import Wire, status_to_numpy
+    from netcode_amd.pipeline import HostPipeline
+    k, r = 16, 6
+    stride = (S + 15) // 16 * 16
+    src, lens = make_sources(G, k, S, stride, seed=G + S, ragged=True)
+    mask = loss_mixed_m(G, k, r, seed=G + S + 1)
+    g = np.arange(G, dtype=np.uint64)
+    sid = ((2**32 - 3 * k + g * k) & 0xFFFFFFFF).astype(np.uint32)
+    rid = ((2**32 - 2 * r + g * r) & 0xFFFFFFFF).astype(np.uint32)
+    orep, orsz = O.encode_batch(src, lens, k, r, sid, rid)
+    lost = src.copy()
+    lost[mask == 0] = 0
+    llen = lens * (mask != 0)
+    oout, olen, ost = O.decode_batch(lost, llen, mask, orep, orsz, np.ones((G, r), np.uint8), sid, rid)
+    sps = Wire.source_packet_bytes(stride)
+    pk, pl, first = [], [], [0]
+    for gi in range(G):
+        for i in range(k):
+            if mask[gi, i]:
+                p = O.write_source_packet(int(sid[gi]) + i, src[gi, i, :lens[gi, i]])
+                pk.append(np.frombuffer(p.ljust(sps, b"\0"), np.uint8))
+                pl.append(len(p))
+        first.append(len(pk))
+    h_rxp = torch.from_numpy(np.stack(pk)).pin_memory()
+    h_rxl = torch.tensor(pl, dtype=torch.int32).pin_memory()
+    rps = Wire.repair_packet_bytes(k, stride)
+    h_rep_pkts = torch.zeros((G * r, rps), dtype=torch.uint8).pin_memory()
+    h_rep_len = torch.zeros((G * r,), dtype=torch.int32).pin_memory()
+    n_lost = int((mask == 0).sum())
+    h_rec = torch.full((max(n_lost, 1), stride), 0xAB, dtype=torch.uint8).pin_memory()
+    h_dec_len = torch.zeros((G, k), dtype=torch.int16).pin_memory()
+    h_st = torch.zeros((G, 12), dtype=torch.uint8).pin_memory()
+    d_sid = torch.from_numpy(sid.view(np.int32).copy()).to(gpu)
+    d_rid = torch.from_numpy(rid.view(np.int32).copy()).to(gpu)
+    p = HostPipeline(k, r, stride, chunk, gpu, depth)
+    p.encode_decode_wire(pinned(src), pinned(lens), h_rep_pkts, h_rep_len, h_rxp, h_rxl,
+                         torch.tensor(first), pinned(mask), h_rec[:n_lost], h_dec_len, h_st, sid, rid,
+                         d_sid, d_rid)
+    torch.cuda.synchronize(gpu)
+    ids = lambda gi: (sid[gi].astype(np.uint64) + np.arange(k, dtype=np.uint64)) & 0xFFFFFFFF
+    for gi in range(G):
+        L = int(lens[gi].max())
+        for j in range(r):
+            ref = O.write_repair_packet(int(rid[gi]) + j, orep[gi, j, :L], ids(gi), int(orsz[gi, j]))
+            n = int(h_rep_len[gi * r + j])
+            assert h_rep_pkts[gi * r + j, :n].numpy().tobytes() == ref, (gi, j)
+    st = status_to_numpy(h_st)
+    assert (st == ost).all()
+    dec = (ost["state"] == 0)
+    lost_gen = np.nonzero(mask == 0)[0]
+    sel = dec[lost_gen]
+    assert (h_rec[:n_lost].numpy()[sel] == oout[mask == 0][sel]).all()
+    assert (h_dec_len.numpy().view(np.uint16)[mask == 0][sel] == olen[mask == 0][sel]).all()

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
   __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];   // tables of c
   __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
   __shared__ __attribute__((aligned(16))) u32x4 rec[kPanel][9];      // step records
+  __shared__ __attribute__((aligned(16))) u32x4 rec_scratch[64];     // the record stores of lanes >= 9
   __shared__ uint32_t stopv[2];                                      // owner's stop step per phase
   __shared__ uint32_t cm[2];                                         // election masks per phase
   __shared__ uint32_t ne[16];                                        // wave has eligible rows
@@ -167,17 +168,21 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
     }
   };
   // the owner's form: the row's table tf (of its column-s byte) was fetched at the start of the
-  // step, before the record exists, and the pivot row takes the record by a select, not a branch
-  auto apply_own = [&](int s, bool pivot, const u32x4 tf, uint32_t tf4) {
+  // step, before the record exists; the record comes as uniform dwords (v_readlane from the lanes
+  // that normalised it, selectors formed on the scalar unit) instead of a round trip through LDS,
+  // and the pivot row takes it by a select, not a branch
+  auto apply_own = [&](int s, bool pivot, const u32x4 tf, uint32_t tf4, const uint32_t (&rv)[9],
+                       bool go) {
     const int q = s >> 2;
     auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
-      const u32x4 c4 = rec[s][e];
-      const uint32_t upd = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
-                                                       __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
-                           __builtin_amdgcn_perm(tf4, tf4, c4[3]);
-      v[wd(e)] = pivot ? c4[0] : upd;
+      const uint32_t c = rv[e];
+      const uint32_t upd = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c & 0x07070707u),
+                                                       __builtin_amdgcn_perm(tf[3], tf[2], (c >> 3) & 0x07070707u),
+                                                       0x96) ^
+                           __builtin_amdgcn_perm(tf4, tf4, (c >> 6) & 0x03030303u);
+      v[wd(e)] = go ? (pivot ? c : upd) : v[wd(e)];
     }
   };
 
@@ -185,10 +190,15 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
   for (uint32_t phase = 0;; ++phase) {
     const uint32_t par = phase & 1u;
     if (w == owner) {                                    // wave-uniform: run ahead from step t
-      uint32_t stop = kPanel;
+      // One basic block for the whole phase: no branch per step (a step before t, or after the
+      // owner ran out of candidates, computes and discards), so the scheduler can start step s+1's
+      // table gathers while step s's other row words are still being updated.  The record is
+      // stored through an address select (lanes >= 9 write a scratch slot) and the pivot rows are
+      // kept in lane s and stored once at the end of the phase.
+      uint32_t stop = kPanel;                            // uniform
+      uint32_t pivs = 0;                                 // lane s: pivot row of step s
 #pragma unroll
       for (int s = 0; s < static_cast<int>(kPanel); ++s) {
-        if (s < static_cast<int>(t)) continue;
         const int q = s >> 2, sh = 8 * (s & 3);
         auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
         const uint32_t f = (v[q] >> sh) & 0xFFu;
@@ -199,8 +209,10 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         const u32x4 tl = *reinterpret_cast<const u32x4*>(&pinv_t[f][0]);
         const uint32_t tl4 = pinv_t[f][4];
         const uint64_t b = __ballot(elig && f != 0);
-        if (b == 0) { stop = s; break; }
-        const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
+        const bool act = static_cast<uint32_t>(s) >= t && stop == kPanel;   // uniform
+        const bool go = act && b != 0;
+        stop = (act && b == 0) ? static_cast<uint32_t>(s) : stop;
+        const uint32_t first = b != 0 ? static_cast<uint32_t>(__ffsll(static_cast<long long>(b)) - 1) : 0u;
         uint32_t x = 0;
 #pragma unroll
         for (int e = 0; e < 9; ++e) {
@@ -214,22 +226,26 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         ti[2] = __builtin_amdgcn_readlane(tl[2], first);
         ti[3] = __builtin_amdgcn_readlane(tl[3], first);
         const uint32_t ti4 = __builtin_amdgcn_readlane(tl4, first);
-        if (lane < 9) {
-          const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);
+        const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);   // lanes 0..8: the record
+        {                                                // for the other waves (after the barrier)
           u32x4 o;
           o[0] = nv;
           o[1] = nv & 0x07070707u;
           o[2] = (nv >> 3) & 0x07070707u;
           o[3] = (nv >> 6) & 0x03030303u;
-          rec[s][lane] = o;
+          u32x4* dst = (go && lane < 9) ? &rec[s][lane] : &rec_scratch[lane];
+          *dst = o;
         }
-        __builtin_amdgcn_wave_barrier();                 // this wave's record writes before its reads
-        const uint32_t prow = w * 64u + first;
-        if (lane == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + s] = prow;
-        const bool me = lane == first;
-        apply_own(s, me, tf, tf4);
-        if (me) { chosen = true; elig = false; }
+        uint32_t rv[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) rv[e] = __builtin_amdgcn_readlane(nv, e);
+        pivs = (go && lane == static_cast<uint32_t>(s)) ? w * 64u + first : pivs;
+        const bool me = go && lane == first;
+        apply_own(s, me, tf, tf4, rv, go);
+        chosen = chosen || me;
+        elig = elig && !me;
       }
+      if (lane >= t && lane < stop) a.piv[static_cast<size_t>(g) * np + a.c0 + lane] = pivs;
       if (lane == 0) stopv[par] = stop;
     }
     __syncthreads();

@@ -20,7 +20,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -747,9 +749,9 @@ __global__ __launch_bounds__(256) void gf_mac(MacArgs a)
 // c * x for the four bytes of x with a per-lane coefficient table (v_perm 3/3/2 split).
 __device__ __forceinline__ uint32_t mul4(const uint32_t* t, uint32_t x)
 {
-  return __builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u) ^
-         __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
-         __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
+  return bxor3(__builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u),
+               __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u),
+               __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u));
 }
 
 struct PrepArgs {
@@ -1638,8 +1640,9 @@ __device__ __forceinline__ void set_byte_dyn(uint32_t (&v)[W], uint32_t i, uint3
 }
 
 // Gauss-Jordan step for column P (compile-time, so every register index is static): false when
-// column P has no nonzero at or below row P (M singular).
-template <int W, int P>
+// column P has no nonzero at or below row P (M singular).  FM: m == 4 * W (every row word live),
+// so the per-word guards go away.
+template <int W, int P, bool FM>
 __device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const uint32_t (*ptab)[8])
 {
   constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -1677,19 +1680,19 @@ __device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const ui
   F[pw] ^= 1u << ps;
 #pragma unroll
   for (int w = 0; w < W; ++w)
-    if (4u * w < m) col[w] ^= mul4(ty, F[w]);
+    if (FM || 4u * w < m) col[w] ^= mul4(ty, F[w]);
   return true;
 }
 
-template <int W, int P, int RM>
+template <int W, int P, int RM, bool FM>
 __device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], uint32_t m, const uint32_t (*ptab)[8])
 {
   if constexpr (P == RM) {
     return true;
   } else {
-    if (static_cast<uint32_t>(P) >= m) return true;
-    if (!gj_step<W, P>(col, m, ptab)) return false;
-    return gj_pivots<W, P + 1, RM>(col, m, ptab);
+    if (!FM && static_cast<uint32_t>(P) >= m) return true;
+    if (!gj_step<W, P, FM>(col, m, ptab)) return false;
+    return gj_pivots<W, P + 1, RM, FM>(col, m, ptab);
   }
 }
 
@@ -1704,6 +1707,17 @@ extern "C" int ntc_dbg_plan_clock(uint64_t* out, uint32_t n)
 #define DBG_CLK(slot)
 #endif
 
+// A kernel-argument field loaded where it is used (the argument block starts the kernarg segment):
+// the opaque offset keeps the compiler from hoisting every field to the kernel entry and holding
+// them in SGPRs across the unrolled Gauss-Jordan steps, where they were spilled.
+template <typename T>
+__device__ __forceinline__ T late_arg(uint32_t off)
+{
+  asm volatile("" : "+s"(off));
+  return const_load<T>(reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())) + off);
+}
+#define NTC_PLAN_ARG(field) late_arg<decltype(PlanArgs::field)>(offsetof(PlanArgs, field))
+
 template <int RM>
 __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 {
@@ -1713,8 +1727,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
   __shared__ uint16_t s_miss[kPlanWaves][RM];
   __shared__ uint16_t s_recv[kPlanWaves][RM];
-  // M^-1 column q as the three v_perm selector words per dword (bits 0-2, 3-5, 6-7 of each byte)
-  __shared__ __attribute__((aligned(16))) uint32_t s_minvS[kPlanWaves][RM][3][W];
+  // scratch of the rank screening: received rows x (W + 1) dwords
+  __shared__ __attribute__((aligned(16))) uint32_t s_scr[kPlanWaves][RM * (W + 1)];
   {
     const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
@@ -1727,7 +1741,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   if (g >= a.G) return;
   uint16_t* miss = s_miss[wv];
   uint16_t* recv = s_recv[wv];
-  uint32_t (*minvS)[3][W] = s_minvS[wv];
+  uint32_t* scr = s_scr[wv];
   auto wave_sync = [] {    // LDS written by some lanes, read by others of the same wave
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1817,12 +1831,12 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
     // candidate (decoder.cc:448-468 tries t = m, m+1, ... in turn).  {first m-1 repairs} + {t} is
     // invertible iff the first m-1 rows are independent and row t lies outside their span: a
     // forward elimination of all received rows over the m missing columns (lane = row, rows in
-    // this wave's minvS scratch, free until a plan is emitted), pivots from rows 0..m-2 only,
+    // this wave's LDS scratch), pivots from rows 0..m-2 only,
     // leaves each candidate reduced against that basis; the first nonzero one is where the
     // reference stops.  Returns that candidate's index, or nrecv when every candidate fails.
     auto screen_candidates = [&]() -> uint32_t {
       constexpr uint32_t SP = W + 1;                   // odd dword pitch
-      uint32_t* S = &minvS[0][0][0];
+      uint32_t* S = scr;
       const uint32_t nwl = (m + 3) / 4;
       if (lane < nrecv) {
         for (uint32_t w = 0; w < nwl; ++w) {
@@ -1887,7 +1901,11 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
       for (int w = 0; w < W; ++w) col[w] = orig[w];
       set_byte_dyn<W>(col, m - 1, ct | byte_dyn<W>(orig, m - 1));
-      if (gj_pivots<W, 0, RM>(col, m, ptab)) { ok = true; break; }
+      if (m == static_cast<uint32_t>(RM) ? gj_pivots<W, 0, RM, true>(col, m, ptab)
+                                         : gj_pivots<W, 0, RM, false>(col, m, ptab)) {
+        ok = true;
+        break;
+      }
       if (t == m - 1 && t + 1 < nrecv) t = screen_candidates() - 1;   // the loop's ++t: next
     }
 #ifdef NTC_PLAN_CLOCK
@@ -1906,11 +1924,11 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       st.nb_useless = static_cast<uint16_t>(nrecv - 1 - t);
       st.last_repair = recv[t];
       mm = m;
-      const uint32_t rp = a.rp;
-      uint16_t* pin = a.plan_in + static_cast<size_t>(g) * k;
-      uint8_t* pc = a.plan_coef + static_cast<size_t>(g) * k * rp;
-      uint16_t* pout = a.plan_out + static_cast<size_t>(g) * rp;
-      uint16_t* slen = a.src_len + static_cast<size_t>(g) * k;
+      const uint32_t rp = NTC_PLAN_ARG(rp);
+      uint16_t* pin = NTC_PLAN_ARG(plan_in) + static_cast<size_t>(g) * k;
+      uint8_t* pc = NTC_PLAN_ARG(plan_coef) + static_cast<size_t>(g) * k * rp;
+      uint16_t* pout = NTC_PLAN_ARG(plan_out) + static_cast<size_t>(g) * rp;
+      uint16_t* slen = NTC_PLAN_ARG(src_len) + static_cast<size_t>(g) * k;
       // plan row of input position `pos`: the rp coefficient bytes
       auto emit = [&](uint32_t pos, const uint32_t (&v)[W]) {
         uint32_t* d = reinterpret_cast<uint32_t*>(pc + static_cast<size_t>(pos) * rp);
@@ -1918,6 +1936,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         for (int w = 0; w < W; ++w)
           if (4u * w < rp) d[w] = v[w];
       };
+      // the rest in two versions: FM (m == RM: every row word live, no per-word guards) or not
+      auto emit_phase = [&](auto fm_c) {
+      constexpr bool FM = decltype(fm_c)::value;
       uint32_t LO[W], HI[W];     // this lane's decoded-size terms, low and high length bytes
 #pragma unroll
       for (int w = 0; w < W; ++w) LO[w] = HI[w] = 0;
@@ -1927,7 +1948,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         tab(len >> 8, th);
 #pragma unroll
         for (int w = 0; w < W; ++w)
-          if (4u * w < m) {
+          if (FM || 4u * w < m) {
             const uint32_t s0 = v[w] & 0x07070707u, s1 = (v[w] >> 3) & 0x07070707u;
             const uint32_t s2 = (v[w] >> 6) & 0x03030303u;
             LO[w] ^= xor3(__builtin_amdgcn_perm(tl[1], tl[0], s0), __builtin_amdgcn_perm(tl[3], tl[2], s1),
@@ -1938,7 +1959,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       };
       // input row address of plan position `pos` (plan_rows' layout: k entries, then kBsRing
       // copies of the last one, read by the MAC's prefetch)
-      uint64_t* rows_g = a.rows_out ? a.rows_out + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
+      uint64_t* const rows_o = NTC_PLAN_ARG(rows_out);
+      uint64_t* rows_g = rows_o ? rows_o + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
       auto put_row = [&](uint32_t pos, const uint8_t* row) {
         if (!rows_g) return;
         const uint64_t v = reinterpret_cast<uint64_t>(row);
@@ -1958,14 +1980,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         const uint32_t q = lane - m;
         const uint32_t rq = rq_l;
         pin[q] = static_cast<uint16_t>(k + rq);
-        put_row(q, a.rows_rep + (static_cast<uint64_t>(g) * r + rq) * a.rows_stride);
+        put_row(q, NTC_PLAN_ARG(rows_rep) + (static_cast<uint64_t>(g) * r + rq) * NTC_PLAN_ARG(rows_stride));
         emit(q, col);
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          minvS[q][0][w] = col[w] & 0x07070707u;
-          minvS[q][1][w] = (col[w] >> 3) & 0x07070707u;
-          minvS[q][2][w] = (col[w] >> 6) & 0x03030303u;
-        }
         size_terms(rsz_l, col);
       }
       if (lane < rp) pout[lane] = lane < m ? miss[lane] : 0;
@@ -1980,7 +1996,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         if (got) {
           const uint32_t pos = pos_base + __popcll(b & lt);
           pin[pos] = static_cast<uint16_t>(j);
-          put_row(pos, a.rows_src + (static_cast<uint64_t>(g) * k + j) * a.rows_stride);
+          put_row(pos, NTC_PLAN_ARG(rows_src) + (static_cast<uint64_t>(g) * k + j) * NTC_PLAN_ARG(rows_stride));
           const uint32_t Sj = sidb + j + 1u;
           uint32_t acc[W];
 #pragma unroll
@@ -1997,20 +2013,18 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             uint32_t tc[5];
 #pragma unroll
             for (int e = 0; e < 5; ++e) tc[e] = tn[e];
-            // column q's selector words: 3 x W dwords, read whole (16-byte broadcast loads;
-            // words past m are unused)
+            // column q's selector words, uniform: M^-1 column q is lane m + q's col[] (read
+            // across lanes, v_readlane works whatever EXEC holds), its v_perm selectors formed on
+            // the scalar unit.  Broadcast LDS reads of them (6 x 16 B per lane and q) saturated
+            // the CU's LDS with 16 waves in this loop.
             uint32_t sq[3][W];
-            if constexpr ((3 * W) % 4 == 0) {     // rows of 16-byte multiples (RM >= 16)
-              const u32x4* sq4 = reinterpret_cast<const u32x4*>(&minvS[q][0][0]);
 #pragma unroll
-              for (int e = 0; e < 3 * W / 4; ++e) {
-                const u32x4 v4 = sq4[e];
-#pragma unroll
-                for (int f = 0; f < 4; ++f) sq[(4 * e + f) / W][(4 * e + f) % W] = v4[f];
-              }
-            } else {
-#pragma unroll
-              for (int e = 0; e < 3 * W; ++e) sq[e / W][e % W] = minvS[q][e / W][e % W];
+            for (int w = 0; w < W; ++w) {
+              if (!(FM || 4u * w < m)) continue;
+              const uint32_t cw = __builtin_amdgcn_readlane(col[w], m + q);
+              sq[0][w] = cw & 0x07070707u;
+              sq[1][w] = (cw >> 3) & 0x07070707u;
+              sq[2][w] = (cw >> 6) & 0x03030303u;
             }
             if (q + 1 < mq) {
               const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q + 1);
@@ -2018,7 +2032,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             }
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              if (4u * w < m)
+              if (FM || 4u * w < m)
                 acc[w] ^= xor3(__builtin_amdgcn_perm(tc[1], tc[0], sq[0][w]),
                                __builtin_amdgcn_perm(tc[3], tc[2], sq[1][w]),
                                __builtin_amdgcn_perm(tc[4], tc[4], sq[2][w]));
@@ -2033,7 +2047,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
         for (int w = 0; w < W; ++w)
-          if (4u * w < m) {
+          if (FM || 4u * w < m) {
             LO[w] ^= __shfl_xor(LO[w], off);
             HI[w] ^= __shfl_xor(HI[w], off);
           }
@@ -2041,11 +2055,14 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         const uint32_t lo = byte_dyn<W>(LO, lane), hi = byte_dyn<W>(HI, lane);
         slen[miss[lane]] = static_cast<uint16_t>(lo | (hi << 8));
       }
+      };
+      if (m == static_cast<uint32_t>(RM)) emit_phase(std::true_type{});
+      else emit_phase(std::false_type{});
     }
   }
   if (lane == 0) {
-    a.plan_m[g] = static_cast<uint16_t>(mm);
-    a.status[g] = st;
+    NTC_PLAN_ARG(plan_m)[g] = static_cast<uint16_t>(mm);
+    NTC_PLAN_ARG(status)[g] = st;
 #ifdef NTC_PLAN_CLOCK
     g_dbg_clk[8 * g + 0] = dbg_t0;
     g_dbg_clk[8 * g + 3] = wall_clock64();

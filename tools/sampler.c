@@ -4,7 +4,7 @@
  * /proc/self/maps, to $NTC_SAMPLER_OUT (default /tmp/ntc_samples.txt).  tools/sampler_report.py
  * turns the file into a flat profile (self) and an inclusive one (self + callers).
  *
- * build: gcc -O2 -shared -fPIC -o /tmp/libsampler.so tools/sampler.c
+ * build: gcc -O2 -shared -fPIC -o /tmp/libsampler.so tools/sampler.c -lrt
  */
 #define _GNU_SOURCE
 #include <signal.h>
@@ -13,13 +13,16 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/time.h>
+#include <time.h>
 #include <ucontext.h>
 
 #define MAXS (1 << 21)
 #define DEPTH 4
 static uintptr_t g_pc[MAXS][DEPTH];
 static volatile long g_n = 0;
-static uintptr_t g_stk_lo = 0, g_stk_hi = 0;   /* main thread stack: frames are walked only inside */
+static uintptr_t g_stk_lo = 0, g_stk_hi = 0;
+static timer_t g_timer;
+static int g_have_timer = 0;   /* main thread stack: frames are walked only inside */
 
 static void on_prof(int sig, siginfo_t* si, void* uc_)
 {
@@ -58,12 +61,25 @@ __attribute__((constructor)) static void start(void)
   sa.sa_sigaction = on_prof;
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigaction(SIGPROF, &sa, NULL);
-  struct itimerval it = {{0, 100}, {0, 100}};
-  setitimer(ITIMER_PROF, &it, NULL);
+  /* a wall-clock POSIX timer (hrtimer): CPU-time timers tick at the kernel HZ here (a few ms);
+   * profile a single busy thread */
+  struct sigevent sev;
+  memset(&sev, 0, sizeof sev);
+  sev.sigev_notify = SIGEV_SIGNAL;
+  sev.sigev_signo = SIGPROF;
+  if (timer_create(CLOCK_MONOTONIC, &sev, &g_timer) == 0) {
+    struct itimerspec its = {{0, 100000}, {0, 100000}};
+    timer_settime(g_timer, 0, &its, NULL);
+    g_have_timer = 1;
+  } else {
+    struct itimerval it = {{0, 100}, {0, 100}};
+    setitimer(ITIMER_PROF, &it, NULL);
+  }
 }
 
 __attribute__((destructor)) static void stop(void)
 {
+  if (g_have_timer) timer_delete(g_timer);
   struct itimerval it = {{0, 0}, {0, 0}};
   setitimer(ITIMER_PROF, &it, NULL);
   const char* path = getenv("NTC_SAMPLER_OUT");

@@ -576,7 +576,9 @@ def per_packet_main(a):
                        ("flows", "c_items", "size", "window", "rate", "loss")}},
             "value_note": "C-level driver (tools/pp_driver.c), GPU region ops batched across flows "
                           "(ntc_batch_t); packets encoded + packets received, over encode + "
-                          "decode time; best of the interleaved runs of each leg (all_runs_s)",
+                          "decode time; best of the interleaved runs of each leg (all_runs_s); "
+                          "both legs copy each item in inside the loop and write into "
+                          "application stores sized and paged in before the clock",
             "c_level": {"gpu_batched": c_gpu["batched"], "gpu_immediate": c_gpu["immediate"],
                         "cpu_oracle": c_cpu},
             "cpu_baseline": {"value": c_cpu["packets_per_s"], "unit": "packets/s", "cores": 1,

@@ -658,18 +658,22 @@ struct Writer {
   void ids(const std::vector<uint32_t>& v)      // packetizer.hh:263-309
   {
     if (v.empty()) { u16(0); return; }
-    std::vector<std::pair<uint8_t, uint16_t>> rle;
-    size_t c = 1;
-    while (c < v.size()) {
-      uint8_t run = 1;
-      const uint32_t d = v[c] - v[c - 1];
-      while (c + 1 < v.size() && v[c + 1] - v[c] == d && run < 255) { ++run; ++c; }
-      rle.emplace_back(run, static_cast<uint16_t>(d));
-      ++c;
-    }
-    u16(static_cast<uint16_t>(rle.size() + 1));
+    // runs of equal differences: counted first (the count leads), then written
+    auto runs = [&v](auto&& emit) {
+      size_t c = 1;
+      while (c < v.size()) {
+        uint8_t run = 1;
+        const uint32_t d = v[c] - v[c - 1];
+        while (c + 1 < v.size() && v[c + 1] - v[c] == d && run < 255) { ++run; ++c; }
+        emit(run, static_cast<uint16_t>(d));
+        ++c;
+      }
+    };
+    size_t nr = 0;
+    runs([&nr](uint8_t, uint16_t) { ++nr; });
+    u16(static_cast<uint16_t>(nr + 1));
     u32(v[0]);
-    for (const auto& p : rle) { u8(p.first); u16(p.second); }
+    runs([this](uint8_t run, uint16_t d) { u8(run); u16(d); });
   }
   void end() { if (!buf) h.send_packet(h.context); }
 };
@@ -921,6 +925,137 @@ class Encoder {
   uint32_t cur_sid_ = 0, cur_rid_ = 0;
   size_t nb_repairs_ = 0, nb_acks_ = 0, nb_sources_ = 0;
   uint16_t nb_sent_packets_ = 0;
+};
+
+// ------------------------------------------------------------------------ flow containers ----
+// A decoder's state spans one window of ids (tens of entries), inserted mostly at the back and
+// dropped from the front: sorted vectors, not node-based trees -- no allocation per packet once the
+// window is warm, and the same ordered iteration as the reference's std::map / std::set.  An
+// insert or erase invalidates iterators and references into the container (the Decoder re-finds
+// by key after any structural change).
+template <class K, class V>
+class FlatMap {
+ public:
+  using value_type = std::pair<K, V>;
+  using iterator = typename std::vector<value_type>::iterator;
+  using const_iterator = typename std::vector<value_type>::const_iterator;
+  iterator begin() { return v_.begin(); }
+  iterator end() { return v_.end(); }
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  void clear() { v_.clear(); }
+  iterator lower_bound(K k)
+  {
+    if (v_.empty() || v_.back().first < k) return v_.end();        // the common case: a new id
+    return std::lower_bound(v_.begin(), v_.end(), k, [](const value_type& a, K b) { return a.first < b; });
+  }
+  iterator find(K k)
+  {
+    auto it = lower_bound(k);
+    return it != v_.end() && it->first == k ? it : v_.end();
+  }
+  size_t count(K k) { return find(k) != v_.end(); }
+  std::pair<iterator, bool> emplace(K k, V&& v)
+  {
+    auto it = lower_bound(k);
+    if (it != v_.end() && it->first == k) return {it, false};
+    return {v_.emplace(it, k, std::move(v)), true};
+  }
+  V& operator[](K k)
+  {
+    auto it = lower_bound(k);
+    if (it == v_.end() || it->first != k) it = v_.emplace(it, k, V());
+    return it->second;
+  }
+  iterator erase(iterator it) { return v_.erase(it); }
+  iterator erase(iterator a, iterator b) { return v_.erase(a, b); }
+  size_t erase(K k)
+  {
+    auto it = find(k);
+    if (it == v_.end()) return 0;
+    v_.erase(it);
+    return 1;
+  }
+
+ private:
+  std::vector<value_type> v_;
+};
+
+// The in-order decoder's ids held back behind a gap.
+class OrderedIds {
+ public:
+  using iterator = std::vector<uint32_t>::iterator;
+  iterator begin() { return v_.begin(); }
+  iterator end() { return v_.end(); }
+  bool empty() const { return v_.empty(); }
+  iterator find(uint32_t x)
+  {
+    auto it = std::lower_bound(v_.begin(), v_.end(), x);
+    return it != v_.end() && *it == x ? it : v_.end();
+  }
+  iterator erase(iterator it) { return v_.erase(it); }
+  void insert(uint32_t x)
+  {
+    if (v_.empty() || v_.back() < x) { v_.push_back(x); return; }
+    auto it = std::lower_bound(v_.begin(), v_.end(), x);
+    if (*it != x) v_.insert(it, x);
+  }
+
+ private:
+  std::vector<uint32_t> v_;
+};
+
+// A sorted set of ids; up to kInline of them without a heap block (a missing source is usually
+// covered by one to three repairs).
+class IdSet {
+ public:
+  static constexpr uint32_t kInline = 6;
+  IdSet() = default;
+  IdSet(const IdSet& o) : n_(o.n_), big_(o.big_) { std::copy(o.in_, o.in_ + kInline, in_); }
+  IdSet(IdSet&& o) noexcept : n_(o.n_), big_(std::move(o.big_)) { std::copy(o.in_, o.in_ + kInline, in_); o.n_ = 0; }
+  IdSet& operator=(IdSet&& o) noexcept
+  {
+    n_ = o.n_;
+    big_ = std::move(o.big_);
+    std::copy(o.in_, o.in_ + kInline, in_);
+    o.n_ = 0;
+    return *this;
+  }
+  const uint32_t* begin() const { return big_.empty() ? in_ : big_.data(); }
+  const uint32_t* end() const { return begin() + n_; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  void insert(uint32_t x)
+  {
+    const uint32_t* b = begin();
+    const size_t i = static_cast<size_t>(std::lower_bound(b, b + n_, x) - b);
+    if (i < n_ && b[i] == x) return;
+    if (big_.empty() && n_ < kInline) {
+      std::copy_backward(in_ + i, in_ + n_, in_ + n_ + 1);
+      in_[i] = x;
+    } else {
+      if (big_.empty()) big_.assign(in_, in_ + n_);
+      big_.insert(big_.begin() + static_cast<std::ptrdiff_t>(i), x);
+    }
+    ++n_;
+  }
+  void erase(uint32_t x)
+  {
+    uint32_t* b = big_.empty() ? in_ : big_.data();
+    uint32_t* e = b + n_;
+    uint32_t* it = std::lower_bound(b, e, x);
+    if (it == e || *it != x) return;
+    if (big_.empty()) std::copy(it + 1, e, it);
+    else big_.erase(big_.begin() + (it - b));
+    --n_;
+  }
+
+ private:
+  uint32_t n_ = 0;
+  uint32_t in_[kInline] = {};
+  std::vector<uint32_t> big_;  // past kInline ids (then the ids live here)
 };
 
 // ============================================================================== decoder ====
@@ -1213,7 +1348,7 @@ class Decoder {
     }
     auto m = missing_.find(src.id);
     if (m != missing_.end()) {
-      const std::set<uint32_t> rids = m->second;
+      const IdSet rids = m->second;
       for (uint32_t rid : rids) {
         auto r = repairs_.find(rid);
         if (r == repairs_.end()) continue;
@@ -1395,10 +1530,10 @@ class Decoder {
   Writer out_;
   ntc_data_handler dh_;
   uint32_t first_missing_ = 0;
-  std::set<uint32_t> ordered_;
-  std::map<uint32_t, Src> sources_;
-  std::map<uint32_t, Rep> repairs_;
-  std::map<uint32_t, std::set<uint32_t>> missing_;
+  OrderedIds ordered_;
+  FlatMap<uint32_t, Src> sources_;
+  FlatMap<uint32_t, Rep> repairs_;
+  FlatMap<uint32_t, IdSet> missing_;
   bool has_last_ = false;
   uint32_t last_id_ = 0;
   size_t nb_useless_ = 0, nb_failed_ = 0, nb_decoded_ = 0;

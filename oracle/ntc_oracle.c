@@ -1719,6 +1719,17 @@ static void pp_push(pp_store* s, const uint8_t* p, size_t n)
   s->off[++s->np] = s->n;
 }
 
+/* the application's stores are sized and paged in before the clock starts (tools/pp_driver.c does
+ * the same) */
+static void pp_reserve(pp_store* s, size_t bytes, size_t items)
+{
+  s->cap = bytes;
+  s->v = (uint8_t*)malloc(bytes);
+  memset(s->v, 0, bytes);
+  s->capp = items + 2;
+  s->off = (size_t*)malloc(s->capp * sizeof(size_t));
+}
+
 static void pp_emit(void* ctx, const uint8_t* p, size_t n) { pp_push((pp_store*)ctx, p, n); }
 static void pp_deliver(void* ctx, uint32_t id, const uint8_t* p, size_t n)
 {
@@ -1747,6 +1758,8 @@ int or_pp_bench(uint32_t F, uint32_t M, uint32_t S, uint32_t W, uint32_t R, uint
   or_encoder** enc = (or_encoder**)calloc(F, sizeof(or_encoder*));
   or_decoder** dec = (or_decoder**)calloc(F, sizeof(or_decoder*));
   for (uint32_t f = 0; f < F; ++f) {
+    pp_reserve(&tx[f], (size_t)M * (S + 16) + (size_t)((R ? M / R : M) + 1) * (2 * S + 256), 2 * (size_t)M + 64);
+    pp_reserve(&rx[f], (size_t)M * S + 4096, (size_t)M + 64);
     enc[f] = or_encoder_new(pp_emit, &tx[f]);
     or_encoder_set_rate(enc[f], R);
     or_encoder_set_window_size(enc[f], W);

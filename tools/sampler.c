@@ -20,6 +20,10 @@
 #define DEPTH 4
 static uintptr_t g_pc[MAXS][DEPTH];
 static volatile long g_n = 0;
+/* NTC_SAMPLER_GATED=1: record only between ntc_sampler_enable(1) and ntc_sampler_enable(0), which
+ * a program under study looks up with dlsym(RTLD_DEFAULT, ...) around its timed region */
+static volatile int g_on = 1;
+void ntc_sampler_enable(int on) { g_on = on; }
 static uintptr_t g_stk_lo = 0, g_stk_hi = 0;
 static timer_t g_timer;
 static int g_have_timer = 0;   /* main thread stack: frames are walked only inside */
@@ -29,7 +33,7 @@ static void on_prof(int sig, siginfo_t* si, void* uc_)
   (void)sig; (void)si;
   ucontext_t* uc = (ucontext_t*)uc_;
   long n = g_n;
-  if (n >= MAXS) return;
+  if (n >= MAXS || !g_on) return;
   g_pc[n][0] = (uintptr_t)uc->uc_mcontext.gregs[REG_RIP];
   uintptr_t* fp = (uintptr_t*)uc->uc_mcontext.gregs[REG_RBP];
   for (int d = 1; d < DEPTH; ++d) {
@@ -48,6 +52,7 @@ static void on_prof(int sig, siginfo_t* si, void* uc_)
 
 __attribute__((constructor)) static void start(void)
 {
+  if (getenv("NTC_SAMPLER_GATED") && atoi(getenv("NTC_SAMPLER_GATED"))) g_on = 0;
   FILE* m = fopen("/proc/self/maps", "r");
   char line[4096];
   while (m && fgets(line, sizeof line, m))

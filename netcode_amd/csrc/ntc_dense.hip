@@ -24,6 +24,7 @@
 // the result is the reference's M^-1 whatever the pivot order, and singularity is a rank property.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -93,6 +94,40 @@ struct PanelArgs {
   uint8_t* ok;         // [G] 0 once singular
 };
 
+// v_perm selector forms of a multiplicand dword x (a record word, a T word, a pivot-row word)
+__device__ __forceinline__ u32x4 sel4(uint32_t x)
+{
+  u32x4 o;
+  o[0] = x;
+  o[1] = x & 0x07070707u;
+  o[2] = (x >> 3) & 0x07070707u;
+  o[3] = (x >> 6) & 0x03030303u;
+  return o;
+}
+
+// c * x, c given by its table (tf, tf4; per lane), x by its selector forms (sel4)
+__device__ __forceinline__ uint32_t mul_sel(const u32x4 tf, uint32_t tf4, const u32x4 c4)
+{
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                     __builtin_amdgcn_perm(tf[3], tf[2], c4[2]),
+                                     __builtin_amdgcn_perm(tf4, tf4, c4[3]), 0x96);
+}
+
+struct PanelSmem {
+  uint32_t perm_t[256][8];                 // tables of c
+  uint32_t pinv_t[256][8];                 // tables of 1/c
+  u32x4 rec[kPanel][9];                    // step records
+  // lookahead (dn_fused): the previous panel's T = B^-1 and its pivot rows' words in this
+  // panel's columns, with their v_perm selectors; partial products of the cooperative pass
+  u32x4 tsel[kPanel][8];
+  u32x4 psel[kPanel][8];
+  uint32_t part[2][8][64];
+  uint32_t part2[2][8][64];
+  uint32_t stopv[2];                       // owner's stop step per phase
+  uint32_t cm[2];                          // election masks per phase
+  uint32_t ne[16];                         // wave has eligible rows
+};
+
 // Panel factorisation with a run-ahead owner wave: pivot order does not change the inverse, so
 // the owner -- one wave that has a candidate -- eliminates the panel's columns on its own 64 rows
 // for as many steps as it keeps finding candidates, writing one record per step (the normalised
@@ -101,88 +136,175 @@ struct PanelArgs {
 // candidates at some column is there an election: every wave reports whether it has one, the
 // lowest such wave becomes the next owner (none: singular).  A random dense matrix needs about one
 // phase per panel, i.e. two barriers per 32 pivots instead of 32.
-__global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
+//
+// LOOKAHEAD (dn_fused): the panel runs in the same launch as the previous panel's update, so its
+// rows' panel columns are not in memory yet.  The block derives them for the owner wave's 64 rows
+// from the pre-update matrix -- W_i = X_i[prev panel] * T, then X_i[panel] ^= sum_t W_i[t] *
+// X[piv_t][panel], the update's own arithmetic, split over all waves -- and the other waves derive
+// their own rows only if the owner does not finish the panel alone (an election).
+template <bool LOOKAHEAD>
+__device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uint32_t g, uint32_t i,
+                                          uint32_t nthreads)
 {
-  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];   // tables of c
-  __shared__ __attribute__((aligned(16))) uint32_t pinv_t[256][8];   // tables of 1/c
-  __shared__ __attribute__((aligned(16))) u32x4 rec[kPanel][9];      // step records
-  __shared__ __attribute__((aligned(16))) u32x4 rec_scratch[64];     // the record stores of lanes >= 9
-  __shared__ uint32_t stopv[2];                                      // owner's stop step per phase
-  __shared__ uint32_t cm[2];                                         // election masks per phase
-  __shared__ uint32_t ne[16];                                        // wave has eligible rows
-
-  const uint32_t g = blockIdx.x, i = threadIdx.x, lane = i & 63u, w = i >> 6;
+  const uint32_t lane = i & 63u, w = i >> 6, nw = nthreads >> 6;
   const uint32_t np = a.np, P = 2 * np;
   const bool row_ok = i < np;
   const size_t gi = static_cast<size_t>(g) * np + i;
   bool elig = row_ok && a.flag[gi] != 0;
-  for (uint32_t e = i; e < 256 * 8; e += blockDim.x) {
-    perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
-    pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
+  const uint32_t cp = a.c0 - kPanel;                   // LOOKAHEAD: the previous panel's columns
+  for (uint32_t e = i; e < 256 * 8; e += nthreads) {
+    sm.perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+    sm.pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
   }
-  if (i < 2) cm[i] = 0;
+  if (LOOKAHEAD) {
+    const uint32_t* pivp = a.piv + static_cast<size_t>(g) * np + cp;
+    for (uint32_t e = i; e < kPanel * 8; e += nthreads) {
+      const uint32_t s = e >> 3, d = e & 7;
+      const size_t prow = static_cast<size_t>(g) * np + pivp[s];
+      sm.tsel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d));
+      sm.psel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.X + prow * P + a.c0 + 4 * d));
+    }
+  }
+  if (i < 2) sm.cm[i] = 0;
   {
     const uint64_t e0 = __ballot(elig);
-    if (lane == 0) ne[w] = e0 != 0 ? 1u : 0u;
+    if (lane == 0) sm.ne[w] = e0 != 0 ? 1u : 0u;
   }
   const bool live = a.ok[g] != 0;
   __syncthreads();
   if (!live) return;                                   // uniform: a singular generation stops
   uint32_t owner = 0;
-  for (uint32_t q = blockDim.x / 64u; q-- > 0;) owner = ne[q] ? q : owner;
+  for (uint32_t q = nw; q-- > 0;) owner = sm.ne[q] ? q : owner;
   owner = __builtin_amdgcn_readfirstlane(owner);
 
   uint32_t v[16];
-  if (row_ok) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
-    const u32x4 q0 = src[0], q1 = src[1];
-    v[0] = q0[0]; v[1] = q0[1]; v[2] = q0[2]; v[3] = q0[3];
-    v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) v[d] = 0;
+  bool have = !LOOKAHEAD;                              // this wave's rows hold the panel columns
+  if (!LOOKAHEAD) {
+    if (row_ok) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
+      const u32x4 q0 = src[0], q1 = src[1];
+      v[0] = q0[0]; v[1] = q0[1]; v[2] = q0[2]; v[3] = q0[3];
+      v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
+    }
   } else {
+    // the owner's 64 rows, all waves: job (d, h) = word d of W_i (phase 1) and of the panel
+    // columns (phase 2) over the 16 terms of half h
+    const uint32_t orow = owner * 64u + lane;
+    const bool orow_ok = orow < np;
+    const size_t go = static_cast<size_t>(g) * np + (orow_ok ? orow : 0u);
+    u32x4 own0 = {0, 0, 0, 0}, own1 = {0, 0, 0, 0};
+    if (w == owner && orow_ok) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(a.X + go * P + a.c0);
+      own0 = src[0];
+      own1 = src[1];
+    }
+    for (uint32_t job = w; job < 16; job += nw) {
+      const uint32_t d = job & 7u, h = job >> 3;
+      u32x4 x4 = {0, 0, 0, 0};
+      if (orow_ok) x4 = *reinterpret_cast<const u32x4*>(a.X + go * P + cp + 16u * h);
+      uint32_t acc = 0;
 #pragma unroll
-    for (int d = 0; d < 8; ++d) v[d] = 0;
+      for (int s = 0; s < 16; ++s) {
+        const uint32_t b = (x4[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
+        acc ^= mul_sel(tf, sm.perm_t[b][4], sm.tsel[16u * h + s][d]);
+      }
+      sm.part[h][d][lane] = acc;
+    }
+    __syncthreads();
+    for (uint32_t job = w; job < 16; job += nw) {
+      const uint32_t d = job & 7u, h = job >> 3;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t wd = sm.part[0][4u * h + q][lane] ^ sm.part[1][4u * h + q][lane];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t b = (wd >> (8 * k)) & 0xFFu;
+          const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
+          acc ^= mul_sel(tf, sm.perm_t[b][4], sm.psel[16u * h + 4 * q + k][d]);
+        }
+      }
+      sm.part2[h][d][lane] = acc;
+    }
+    __syncthreads();
+    if (w == owner) {
+      const uint32_t x8[8] = {own0[0], own0[1], own0[2], own0[3], own1[0], own1[1], own1[2], own1[3]};
+#pragma unroll
+      for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ sm.part2[0][d][lane] ^ sm.part2[1][d][lane] : 0u;
+      have = true;
+    }
   }
+  // LOOKAHEAD, a wave that is needed after all: its rows' panel columns on its own
+  auto materialise = [&]() {
+    if (have) return;
+    have = true;
+    if (!row_ok) return;
+    // (the rare path: kept small -- a loop over the words, not unrolled)
+    uint32_t wi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t xq = *reinterpret_cast<const uint32_t*>(a.X + gi * P + cp + 4 * q);
 #pragma unroll
-  for (int d = 8; d < 16; ++d) v[d] = 0;
-  bool chosen = false;
-  bool singular = false;
-
-  // row -= f * record s (window of step s), or become record s when this row is its pivot
-  auto apply = [&](int s, bool pivot) {
-    const int q = s >> 2, sh = 8 * (s & 3);
-    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
-    const uint32_t f = (v[q] >> sh) & 0xFFu;
-    if (pivot) {
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = (xq >> (8 * k)) & 0xFFu;
+        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
+        const uint32_t tf4 = sm.perm_t[b][4];
 #pragma unroll
-      for (int e = 0; e < 9; ++e) v[wd(e)] = rec[s][e][0];
-    } else if (f != 0) {
-      const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);
-      const uint32_t tf4 = perm_t[f][4];
+        for (int d = 0; d < 8; ++d) wi[d] ^= mul_sel(tf, tf4, sm.tsel[4 * q + k][d]);
+      }
+    }
+    const u32x4* xc = reinterpret_cast<const u32x4*>(a.X + gi * P + a.c0);
+    const u32x4 c0v = xc[0], c1v = xc[1];
+    v[0] = c0v[0]; v[1] = c0v[1]; v[2] = c0v[2]; v[3] = c0v[3];
+    v[4] = c1v[0]; v[5] = c1v[1]; v[6] = c1v[2]; v[7] = c1v[3];
+#pragma unroll 1
+    for (int q = 0; q < 8; ++q) {
+      uint32_t wq = 0;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) {
-        const u32x4 c4 = rec[s][e];
-        v[wd(e)] = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
-                                               __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
-                   __builtin_amdgcn_perm(tf4, tf4, c4[3]);
+      for (int qq = 0; qq < 8; ++qq) wq = qq == q ? wi[qq] : wq;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = (wq >> (8 * k)) & 0xFFu;
+        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
+        const uint32_t tf4 = sm.perm_t[b][4];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) v[d] ^= mul_sel(tf, tf4, sm.psel[4 * q + k][d]);
       }
     }
   };
+  bool chosen = false;
+  bool singular = false;
+
+  // row -= f * record s (window of step s)
+  auto apply = [&](int s) {
+    const int q = s >> 2, sh = 8 * (s & 3);
+    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
+    const uint32_t f = (v[q] >> sh) & 0xFFu;
+    if (f != 0) {
+      const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[f][0]);
+      const uint32_t tf4 = sm.perm_t[f][4];
+#pragma unroll
+      for (int e = 0; e < 9; ++e) v[wd(e)] ^= mul_sel(tf, tf4, sm.rec[s][e]);
+    }
+  };
   // the owner's form: the row's table tf (of its column-s byte) was fetched at the start of the
-  // step, before the record exists; the record comes as uniform dwords (v_readlane from the lanes
-  // that normalised it, selectors formed on the scalar unit) instead of a round trip through LDS,
-  // and the pivot row takes it by a select, not a branch
-  auto apply_own = [&](int s, bool pivot, const u32x4 tf, uint32_t tf4, const uint32_t (&rv)[9],
-                       bool go) {
+  // step, before the record exists, and the pivot row takes the record by a select, not a branch.
+  // (Round 4 measured two alternatives slower at n = 1024: the record as v_readlane'd uniform
+  // dwords instead of an LDS round trip, 0.888 -> 0.961 ms, and one branch-free basic block per
+  // phase, -> 1.04 ms.)
+  auto apply_own = [&](int s, bool pivot, const u32x4 tf, uint32_t tf4) {
     const int q = s >> 2;
     auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
-      const uint32_t c = rv[e];
-      const uint32_t upd = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c & 0x07070707u),
-                                                       __builtin_amdgcn_perm(tf[3], tf[2], (c >> 3) & 0x07070707u),
-                                                       0x96) ^
-                           __builtin_amdgcn_perm(tf4, tf4, (c >> 6) & 0x03030303u);
-      v[wd(e)] = go ? (pivot ? c : upd) : v[wd(e)];
+      const u32x4 c4 = sm.rec[s][e];
+      const uint32_t upd = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                                       __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
+                           __builtin_amdgcn_perm(tf4, tf4, c4[3]);
+      v[wd(e)] = pivot ? c4[0] : upd;
     }
   };
 
@@ -190,29 +312,22 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
   for (uint32_t phase = 0;; ++phase) {
     const uint32_t par = phase & 1u;
     if (w == owner) {                                    // wave-uniform: run ahead from step t
-      // One basic block for the whole phase: no branch per step (a step before t, or after the
-      // owner ran out of candidates, computes and discards), so the scheduler can start step s+1's
-      // table gathers while step s's other row words are still being updated.  The record is
-      // stored through an address select (lanes >= 9 write a scratch slot) and the pivot rows are
-      // kept in lane s and stored once at the end of the phase.
-      uint32_t stop = kPanel;                            // uniform
-      uint32_t pivs = 0;                                 // lane s: pivot row of step s
+      uint32_t stop = kPanel;
 #pragma unroll
       for (int s = 0; s < static_cast<int>(kPanel); ++s) {
+        if (s < static_cast<int>(t)) continue;
         const int q = s >> 2, sh = 8 * (s & 3);
         auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
         const uint32_t f = (v[q] >> sh) & 0xFFu;
-        const u32x4 tf = *reinterpret_cast<const u32x4*>(&perm_t[f][0]);   // f = 0: all-zero table
-        const uint32_t tf4 = perm_t[f][4];
+        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[f][0]);   // f = 0: all-zero table
+        const uint32_t tf4 = sm.perm_t[f][4];
         // every row's 1/f table too: the pivot's is then read from its lane (readlane), not
         // looked up after the pivot is known
-        const u32x4 tl = *reinterpret_cast<const u32x4*>(&pinv_t[f][0]);
-        const uint32_t tl4 = pinv_t[f][4];
+        const u32x4 tl = *reinterpret_cast<const u32x4*>(&sm.pinv_t[f][0]);
+        const uint32_t tl4 = sm.pinv_t[f][4];
         const uint64_t b = __ballot(elig && f != 0);
-        const bool act = static_cast<uint32_t>(s) >= t && stop == kPanel;   // uniform
-        const bool go = act && b != 0;
-        stop = (act && b == 0) ? static_cast<uint32_t>(s) : stop;
-        const uint32_t first = b != 0 ? static_cast<uint32_t>(__ffsll(static_cast<long long>(b)) - 1) : 0u;
+        if (b == 0) { stop = s; break; }
+        const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
         uint32_t x = 0;
 #pragma unroll
         for (int e = 0; e < 9; ++e) {
@@ -226,37 +341,26 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
         ti[2] = __builtin_amdgcn_readlane(tl[2], first);
         ti[3] = __builtin_amdgcn_readlane(tl[3], first);
         const uint32_t ti4 = __builtin_amdgcn_readlane(tl4, first);
-        const uint32_t nv = mul4(ti[0], ti[1], ti[2], ti[3], ti4, x);   // lanes 0..8: the record
-        {                                                // for the other waves (after the barrier)
-          u32x4 o;
-          o[0] = nv;
-          o[1] = nv & 0x07070707u;
-          o[2] = (nv >> 3) & 0x07070707u;
-          o[3] = (nv >> 6) & 0x03030303u;
-          u32x4* dst = (go && lane < 9) ? &rec[s][lane] : &rec_scratch[lane];
-          *dst = o;
-        }
-        uint32_t rv[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) rv[e] = __builtin_amdgcn_readlane(nv, e);
-        pivs = (go && lane == static_cast<uint32_t>(s)) ? w * 64u + first : pivs;
-        const bool me = go && lane == first;
-        apply_own(s, me, tf, tf4, rv, go);
-        chosen = chosen || me;
-        elig = elig && !me;
+        if (lane < 9) sm.rec[s][lane] = sel4(mul4(ti[0], ti[1], ti[2], ti[3], ti4, x));
+        __builtin_amdgcn_wave_barrier();                 // this wave's record writes before its reads
+        const uint32_t prow = w * 64u + first;
+        if (lane == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + s] = prow;
+        const bool me = lane == first;
+        apply_own(s, me, tf, tf4);
+        if (me) { chosen = true; elig = false; }
       }
-      if (lane >= t && lane < stop) a.piv[static_cast<size_t>(g) * np + a.c0 + lane] = pivs;
-      if (lane == 0) stopv[par] = stop;
+      if (lane == 0) sm.stopv[par] = stop;
     }
     __syncthreads();
-    const uint32_t stop = __builtin_amdgcn_readfirstlane(stopv[par]);
+    const uint32_t stop = __builtin_amdgcn_readfirstlane(sm.stopv[par]);
     // the other waves need the records only to elect (phase incomplete) or to finish rows they
     // gave as pivots in an earlier phase; the trackers of non-pivot rows come from dn_update
     const bool need = stop < kPanel || __ballot(chosen) != 0;
     if (w != owner && need) {
+      materialise();
 #pragma unroll
       for (int s = 0; s < static_cast<int>(kPanel); ++s)
-        if (s >= static_cast<int>(t) && s < static_cast<int>(stop)) apply(s, false);
+        if (s >= static_cast<int>(t) && s < static_cast<int>(stop)) apply(s);
     }
     t = stop;
     if (t >= kPanel) break;
@@ -266,10 +370,10 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
     for (int s = 0; s < static_cast<int>(kPanel); ++s)
       if (s == static_cast<int>(t)) f = (v[s >> 2] >> (8 * (s & 3))) & 0xFFu;
     const uint64_t b = __ballot(elig && f != 0);
-    if (b != 0 && lane == 0) atomicOr(&cm[par], 1u << w);
+    if (b != 0 && lane == 0) atomicOr(&sm.cm[par], 1u << w);
     __syncthreads();
-    const uint32_t m = __builtin_amdgcn_readfirstlane(cm[par]);
-    if (i == 0) cm[par ^ 1u] = 0;                        // next read after two more barriers
+    const uint32_t m = __builtin_amdgcn_readfirstlane(sm.cm[par]);
+    if (i == 0) sm.cm[par ^ 1u] = 0;                     // next read after two more barriers
     if (m == 0) { singular = true; break; }              // uniform
     owner = __ffs(m) - 1;
   }
@@ -291,6 +395,12 @@ __global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
   }
 }
 
+__global__ __launch_bounds__(1024) void dn_panel_ra(PanelArgs a)
+{
+  __shared__ __attribute__((aligned(16))) PanelSmem sm;
+  panel_run<false>(a, sm, blockIdx.x, threadIdx.x, blockDim.x);
+}
+
 struct UpdArgs {
   uint32_t G, np, c0, cs;      // cs: first column to produce
   uint32_t ntiles, nspans;
@@ -302,19 +412,20 @@ struct UpdArgs {
   const uint8_t* ok;
 };
 
-// One wave per (generation, 4-row tile, 256-column span of [cs, 2np)), 4 bytes per lane:
-//   Y[i][c] = keep_i * X[i][c]  XOR  sum_t W[t][i] * X[piv_t][c]
+// One update task (a wave) per (generation, 4-row tile, 256-column span of [cs, 2np)), 4 bytes
+// per lane:  Y[i][c] = keep_i * X[i][c]  XOR  sum_t W[t][i] * X[piv_t][c].
 // Pivot-row slices stream in groups of 8 with the next group's loads in flight; v_perm tables come
 // from an LDS copy (uniform addresses: broadcast reads).  Narrow spans keep >= 2 waves per SIMD
 // at n = 1024 (G = 1), which this latency-bound kernel needs.
-__global__ __launch_bounds__(256) void dn_update(UpdArgs a)
+struct UpdSmem {
+  uint32_t perm_t[256][8];
+  uint32_t tT[16][kPanel * 8];             // per wave: T by step
+};
+
+__device__ __forceinline__ void update_task(const UpdArgs& a, uint32_t task, uint32_t lane, uint32_t* tT,
+                                            const uint32_t (*perm_t)[8])
 {
-  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
-  __shared__ __attribute__((aligned(16))) uint32_t tT_all[4][kPanel * 8];   // per wave: T by step
-  for (uint32_t e = threadIdx.x; e < 256 * 8; e += 256) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t task = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  task = __builtin_amdgcn_readfirstlane(task);
   const uint32_t span = task % a.nspans;
   task /= a.nspans;
   const uint32_t tile = task % a.ntiles;
@@ -337,7 +448,6 @@ __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
   // row j, T staged in this wave's LDS slice.
   uint32_t wv[4 * kUpdRows * 2];
   {
-    uint32_t* tT = tT_all[threadIdx.x >> 6];
     {
       const uint32_t s = lane >> 1, h = lane & 1u;
       const u32x4 q = *reinterpret_cast<const u32x4*>(
@@ -407,6 +517,43 @@ __global__ __launch_bounds__(256) void dn_update(UpdArgs a)
   for (int j = 0; j < kUpdRows; ++j) *reinterpret_cast<uint32_t*>(Yg + static_cast<size_t>(i0 + j) * P + col) = acc[j];
 }
 
+__global__ __launch_bounds__(256) void dn_update(UpdArgs a)        // one task per wave
+{
+  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
+  __shared__ __attribute__((aligned(16))) uint32_t tT_all[4][kPanel * 8];
+  for (uint32_t e = threadIdx.x; e < 256 * 8; e += 256) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+  __syncthreads();
+  update_task(a, blockIdx.x * 4u + (threadIdx.x >> 6), threadIdx.x & 63u, tT_all[threadIdx.x >> 6], perm_t);
+}
+
+struct FusedArgs {
+  PanelArgs pa;                // panel p + 1 (LOOKAHEAD)
+  UpdArgs ua;                  // update of panel p
+  uint32_t nA;                 // blocks [0, nA): one panel per generation; the rest: update tasks
+  uint32_t tpb;                // update tasks (waves) per block
+};
+
+// Panel p + 1 beside the update of panel p, in one launch: the panel's owner chain runs while the
+// other CUs apply panel p (they touch disjoint state: the update reads keep / W / piv of panel p
+// and writes Y; the panel reads X, writes piv of its own columns, flags, the other keep buffer and
+// the trackers of rows not chosen in panel p).
+__global__ __launch_bounds__(1024) void dn_fused(FusedArgs f)
+{
+  __shared__ __attribute__((aligned(16))) union {
+    PanelSmem p;
+    UpdSmem u;
+  } sm;
+  if (blockIdx.x < f.nA) {
+    panel_run<true>(f.pa, sm.p, blockIdx.x, threadIdx.x, blockDim.x);
+    return;
+  }
+  for (uint32_t e = threadIdx.x; e < 256 * 8; e += blockDim.x) sm.u.perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+  __syncthreads();
+  const uint32_t w = threadIdx.x >> 6;
+  if (w >= f.tpb) return;
+  update_task(f.ua, (blockIdx.x - f.nA) * f.tpb + w, threadIdx.x & 63u, sm.u.tT[w], sm.u.perm_t);
+}
+
 // inv[g][t][0..n) = X[g][piv[t]][np .. np + n)  (zeros for a singular generation)
 __global__ __launch_bounds__(256) void dn_gather_inv(uint32_t n, uint32_t np, const uint8_t* __restrict__ X,
                                                      const uint32_t* __restrict__ piv,
@@ -449,6 +596,16 @@ using namespace ntcgpu::dense;
 
 namespace {
 
+// NTC_DENSE_LOOKAHEAD=0: panel and update in separate launches (A/B experiments)
+bool dense_lookahead()
+{
+  static const bool on = [] {
+    const char* v = std::getenv("NTC_DENSE_LOOKAHEAD");
+    return !v || std::atoi(v) != 0;
+  }();
+  return on;
+}
+
 // Blocked Gauss-Jordan of G n x n matrices; on return (stream order) the inverse rows sit in the
 // engine's X buffer (rows permuted by piv) and ok[g] says whether generation g was invertible.
 int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat, hipStream_t st,
@@ -461,31 +618,63 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
   if ((rc = ensure_buf(&e->dn_y, &e->dn_y_cap, xb, "hipMalloc dense Y"))) return rc;
   if ((rc = ensure_buf(&e->dn_w, &e->dn_w_cap, static_cast<size_t>(G) * kPanel * np + 16, "hipMalloc dense W"))) return rc;
   if ((rc = ensure_buf(&e->dn_piv, &e->dn_piv_cap, static_cast<size_t>(G) * np * 4 + 16, "hipMalloc dense piv"))) return rc;
-  if ((rc = ensure_buf(&e->dn_flag, &e->dn_flag_cap, static_cast<size_t>(G) * np * 2 + 16, "hipMalloc dense flags"))) return rc;
+  if ((rc = ensure_buf(&e->dn_flag, &e->dn_flag_cap, static_cast<size_t>(G) * np * 3 + 16, "hipMalloc dense flags"))) return rc;
   if ((rc = ensure_buf(&e->dn_ok, &e->dn_ok_cap, G + 16, "hipMalloc dense ok"))) return rc;
   uint8_t* X = static_cast<uint8_t*>(e->dn_x);
   uint8_t* Y = static_cast<uint8_t*>(e->dn_y);
   uint8_t* flag = static_cast<uint8_t*>(e->dn_flag);
-  uint8_t* keep = flag + static_cast<size_t>(G) * np;
+  // keep flags by panel parity: with lookahead, panel p + 1 writes its own while p's update reads
+  uint8_t* keep[2] = {flag + static_cast<size_t>(G) * np, flag + static_cast<size_t>(G) * np * 2};
   uint8_t* ok = static_cast<uint8_t*>(e->dn_ok);
+  uint8_t* W = static_cast<uint8_t*>(e->dn_w);
+  uint32_t* piv = static_cast<uint32_t*>(e->dn_piv);
   hipLaunchKernelGGL(dn_init, dim3(np, G), dim3(256), 0, st, mat, n, np, X, flag, ok);
   if ((rc = hip_check(hipGetLastError(), "dn_init launch"))) return rc;
   const uint32_t threads = (np + 63) / 64 * 64;
-  for (uint32_t c0 = 0; c0 < np; c0 += kPanel) {
-    PanelArgs pa{np, c0, X, static_cast<uint8_t*>(e->dn_w), static_cast<uint32_t*>(e->dn_piv), flag, keep, ok};
-    hipLaunchKernelGGL(dn_panel_ra, dim3(G), dim3(threads), 0, st, pa);
-    if ((rc = hip_check(hipGetLastError(), "dn_panel launch"))) return rc;
+  const uint32_t npan = np / kPanel;
+  auto upd_args = [&](uint32_t p) {
     UpdArgs ua{};
+    const uint32_t c0 = p * kPanel;
     ua.G = G; ua.np = np; ua.c0 = c0;
     // the A half left of the next panel is never read again; the last panel only needs the I half
     ua.cs = c0 + kPanel < np ? c0 + kPanel : np;
     ua.ntiles = np / kUpdRows;
     ua.nspans = (2 * np - ua.cs + kUpdSpan - 1) / kUpdSpan;
-    ua.X = X; ua.Y = Y; ua.W = static_cast<const uint8_t*>(e->dn_w);
-    ua.piv = static_cast<const uint32_t*>(e->dn_piv); ua.keep = keep; ua.ok = ok;
+    ua.X = X; ua.Y = Y; ua.W = W; ua.piv = piv; ua.keep = keep[p & 1]; ua.ok = ok;
+    return ua;
+  };
+  auto panel_args = [&](uint32_t p) {
+    return PanelArgs{np, p * kPanel, X, W, piv, flag, keep[p & 1], ok};
+  };
+  PanelArgs pa0 = panel_args(0);
+  hipLaunchKernelGGL(dn_panel_ra, dim3(G), dim3(threads), 0, st, pa0);
+  if ((rc = hip_check(hipGetLastError(), "dn_panel launch"))) return rc;
+  for (uint32_t p = 0; p < npan; ++p) {
+    const UpdArgs ua = upd_args(p);
     const uint64_t waves = static_cast<uint64_t>(G) * ua.ntiles * ua.nspans;
-    hipLaunchKernelGGL(dn_update, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(256), 0, st, ua);
-    if ((rc = hip_check(hipGetLastError(), "dn_update launch"))) return rc;
+    if (p + 1 < npan && dense_lookahead()) {
+      // update p and panel p + 1 in one launch; update tasks spread over the CUs the panels leave
+      FusedArgs fa{};
+      fa.pa = panel_args(p + 1);
+      fa.ua = ua;
+      fa.nA = G;
+      const uint32_t nw = threads / 64;
+      const uint64_t spread = G < 240 ? 240 - G : 16;
+      fa.tpb = static_cast<uint32_t>(std::min<uint64_t>(nw, std::max<uint64_t>(1, (waves + spread - 1) / spread)));
+      const uint64_t nb = (waves + fa.tpb - 1) / fa.tpb;
+      hipLaunchKernelGGL(dn_fused, dim3(static_cast<uint32_t>(G + nb)), dim3(threads), 0, st, fa);
+      if ((rc = hip_check(hipGetLastError(), "dn_fused launch"))) return rc;
+    } else {
+      hipLaunchKernelGGL(dn_update, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(256), 0, st, ua);
+      if ((rc = hip_check(hipGetLastError(), "dn_update launch"))) return rc;
+      if (p + 1 < npan) {
+        uint8_t* tmp = X; X = Y; Y = tmp;
+        PanelArgs pa = panel_args(p + 1);
+        hipLaunchKernelGGL(dn_panel_ra, dim3(G), dim3(threads), 0, st, pa);
+        if ((rc = hip_check(hipGetLastError(), "dn_panel launch"))) return rc;
+        continue;
+      }
+    }
     uint8_t* tmp = X; X = Y; Y = tmp;
   }
   *Xout = X;

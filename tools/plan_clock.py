@@ -40,4 +40,13 @@ for name, sel in (("decoded", st == 0), ("singular", st == 3)):
                  "gj_us_p50": us(np.median(t2[sel] - t1[sel])), "gj_us_max": us((t2[sel] - t1[sel]).max()),
                  "emit_us_p50": us(np.median(t3[sel] - t2[sel])),
                  "end_us_max": us(t3[sel].max() - base)}
+# where the waves ran: HW_ID bits 8-15 (CU, SH, SE) + XCC id -> waves per CU and their durations
+hw, xcc = t[:, 5], t[:, 6]
+cu = (xcc << 8) | ((hw >> 8) & 0xFF)
+_, inv, cnt = np.unique(cu, return_inverse=True, return_counts=True)
+load = cnt[inv]
+res["cus"] = int(len(cnt))
+res["waves_per_cu_hist"] = {int(v): int((cnt == v).sum()) for v in np.unique(cnt)}
+res["dur_us_p50_by_cu_waves"] = {int(v): us(float(np.median((t3 - t0)[load == v]))) for v in np.unique(load)}
+res["end_us_max_by_cu_waves"] = {int(v): us(float((t3 - base)[load == v].max())) for v in np.unique(load)}
 print(json.dumps(res))

@@ -58,11 +58,53 @@ __device__ __forceinline__ uint32_t mul4(uint32_t t0, uint32_t t1, uint32_t t2, 
                                      __builtin_amdgcn_perm(t4, t4, (x >> 6) & 0x03030303u), 0x96);
 }
 
+// A v_perm table set in LDS, split by dword so that per-lane gathers spread over the banks: the
+// first four dwords of c's table at a 16-byte pitch (a ds_read_b128 of 16 lanes touches bank
+// group c mod 16), the fifth at a 4-byte pitch (a ds_read_b32 of 32 lanes: bank c mod 32).  The
+// PermTables layout (8 dwords per c) put every b128 gather on c mod 8 and every fifth-dword
+// gather on c mod 4, 2-3x the LDS cycles of this one for random c.
+struct LdsTab {
+  u32x4 a[256];
+  uint32_t b[256];
+};
+
+__device__ __forceinline__ void stage_tab(LdsTab& t, const PermTables& src, uint32_t tid, uint32_t n)
+{
+  for (uint32_t c = tid; c < 256; c += n) {
+    u32x4 v;
+    v[0] = src.w[c][0]; v[1] = src.w[c][1]; v[2] = src.w[c][2]; v[3] = src.w[c][3];
+    t.a[c] = v;
+    t.b[c] = src.w[c][4];
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T const_load(const void* p)
 {
   return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
 }
+
+#ifdef NTC_DENSE_CLOCK
+// Timeline of the lookahead launches (experiment builds only): per launch (index = the panel it
+// factors), the panel block's stamps and the update blocks' first start / last end.
+__device__ unsigned long long g_dn_clk[64 * 8];
+#define DN_CLK(idx, slot)                                                    \
+  do {                                                                       \
+    if (threadIdx.x == 0) g_dn_clk[(idx) * 8 + (slot)] = wall_clock64();     \
+  } while (0)
+extern "C" int ntc_dbg_dense_clock(unsigned long long* out, uint32_t n, int reset)
+{
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dn_clk), n * 8) != hipSuccess) return -1;
+  if (reset) {
+    static unsigned long long init[64 * 8];
+    for (int i = 0; i < 64 * 8; ++i) init[i] = (i % 8 == 6) ? ~0ull : 0ull;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dn_clk), init, sizeof(init)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#else
+#define DN_CLK(idx, slot) do { } while (0)
+#endif
 
 // X[g] = [A | I]: A = mat[g] (n x n) inside an np x np identity.  Row flags: eligible = 1.
 __global__ __launch_bounds__(256) void dn_init(const uint8_t* __restrict__ mat, uint32_t n,
@@ -114,8 +156,8 @@ __device__ __forceinline__ uint32_t mul_sel(const u32x4 tf, uint32_t tf4, const 
 }
 
 struct PanelSmem {
-  uint32_t perm_t[256][8];                 // tables of c
-  uint32_t pinv_t[256][8];                 // tables of 1/c
+  LdsTab perm_t;                           // tables of c
+  LdsTab pinv_t;                           // tables of 1/c
   u32x4 rec[kPanel][9];                    // step records
   // lookahead (dn_fused): the previous panel's T = B^-1 and its pivot rows' words in this
   // panel's columns, with their v_perm selectors; partial products of the cooperative pass
@@ -152,10 +194,9 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
   const size_t gi = static_cast<size_t>(g) * np + i;
   bool elig = row_ok && a.flag[gi] != 0;
   const uint32_t cp = a.c0 - kPanel;                   // LOOKAHEAD: the previous panel's columns
-  for (uint32_t e = i; e < 256 * 8; e += nthreads) {
-    sm.perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
-    sm.pinv_t[e >> 3][e & 7] = dn_pinv.w[e >> 3][e & 7];
-  }
+  if (LOOKAHEAD && g == 0) DN_CLK(a.c0 / kPanel, 0);
+  stage_tab(sm.perm_t, dn_perm, i, nthreads);
+  stage_tab(sm.pinv_t, dn_pinv, i, nthreads);
   if (LOOKAHEAD) {
     const uint32_t* pivp = a.piv + static_cast<size_t>(g) * np + cp;
     for (uint32_t e = i; e < kPanel * 8; e += nthreads) {
@@ -172,6 +213,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
   }
   const bool live = a.ok[g] != 0;
   __syncthreads();
+  if (LOOKAHEAD && g == 0) DN_CLK(a.c0 / kPanel, 1);
   if (!live) return;                                   // uniform: a singular generation stops
   uint32_t owner = 0;
   for (uint32_t q = nw; q-- > 0;) owner = sm.ne[q] ? q : owner;
@@ -208,8 +250,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const uint32_t b = (x4[s >> 2] >> (8 * (s & 3))) & 0xFFu;
-        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
-        acc ^= mul_sel(tf, sm.perm_t[b][4], sm.tsel[16u * h + s][d]);
+        const u32x4 tf = sm.perm_t.a[b];
+        acc ^= mul_sel(tf, sm.perm_t.b[b], sm.tsel[16u * h + s][d]);
       }
       sm.part[h][d][lane] = acc;
     }
@@ -223,8 +265,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const uint32_t b = (wd >> (8 * k)) & 0xFFu;
-          const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
-          acc ^= mul_sel(tf, sm.perm_t[b][4], sm.psel[16u * h + 4 * q + k][d]);
+          const u32x4 tf = sm.perm_t.a[b];
+          acc ^= mul_sel(tf, sm.perm_t.b[b], sm.psel[16u * h + 4 * q + k][d]);
         }
       }
       sm.part2[h][d][lane] = acc;
@@ -236,6 +278,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ sm.part2[0][d][lane] ^ sm.part2[1][d][lane] : 0u;
       have = true;
     }
+    if (g == 0) DN_CLK(a.c0 / kPanel, 2);
   }
   // LOOKAHEAD, a wave that is needed after all: its rows' panel columns on its own
   auto materialise = [&]() {
@@ -250,8 +293,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t b = (xq >> (8 * k)) & 0xFFu;
-        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
-        const uint32_t tf4 = sm.perm_t[b][4];
+        const u32x4 tf = sm.perm_t.a[b];
+        const uint32_t tf4 = sm.perm_t.b[b];
 #pragma unroll
         for (int d = 0; d < 8; ++d) wi[d] ^= mul_sel(tf, tf4, sm.tsel[4 * q + k][d]);
       }
@@ -268,8 +311,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t b = (wq >> (8 * k)) & 0xFFu;
-        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[b][0]);
-        const uint32_t tf4 = sm.perm_t[b][4];
+        const u32x4 tf = sm.perm_t.a[b];
+        const uint32_t tf4 = sm.perm_t.b[b];
 #pragma unroll
         for (int d = 0; d < 8; ++d) v[d] ^= mul_sel(tf, tf4, sm.psel[4 * q + k][d]);
       }
@@ -284,8 +327,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
     auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
     const uint32_t f = (v[q] >> sh) & 0xFFu;
     if (f != 0) {
-      const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[f][0]);
-      const uint32_t tf4 = sm.perm_t[f][4];
+      const u32x4 tf = sm.perm_t.a[f];
+      const uint32_t tf4 = sm.perm_t.b[f];
 #pragma unroll
       for (int e = 0; e < 9; ++e) v[wd(e)] ^= mul_sel(tf, tf4, sm.rec[s][e]);
     }
@@ -319,12 +362,12 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         const int q = s >> 2, sh = 8 * (s & 3);
         auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
         const uint32_t f = (v[q] >> sh) & 0xFFu;
-        const u32x4 tf = *reinterpret_cast<const u32x4*>(&sm.perm_t[f][0]);   // f = 0: all-zero table
-        const uint32_t tf4 = sm.perm_t[f][4];
+        const u32x4 tf = sm.perm_t.a[f];   // f = 0: all-zero table
+        const uint32_t tf4 = sm.perm_t.b[f];
         // every row's 1/f table too: the pivot's is then read from its lane (readlane), not
         // looked up after the pivot is known
-        const u32x4 tl = *reinterpret_cast<const u32x4*>(&sm.pinv_t[f][0]);
-        const uint32_t tl4 = sm.pinv_t[f][4];
+        const u32x4 tl = sm.pinv_t.a[f];
+        const uint32_t tl4 = sm.pinv_t.b[f];
         const uint64_t b = __ballot(elig && f != 0);
         if (b == 0) { stop = s; break; }
         const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
@@ -352,6 +395,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       if (lane == 0) sm.stopv[par] = stop;
     }
     __syncthreads();
+    if (LOOKAHEAD && g == 0 && phase == 0) DN_CLK(a.c0 / kPanel, 3);
     const uint32_t stop = __builtin_amdgcn_readfirstlane(sm.stopv[par]);
     // the other waves need the records only to elect (phase incomplete) or to finish rows they
     // gave as pivots in an earlier phase; the trackers of non-pivot rows come from dn_update
@@ -385,6 +429,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
     a.flag[gi] = elig ? 1 : 0;
     a.keep[gi] = chosen ? 0 : 1;
   }
+  if (LOOKAHEAD && g == 0) DN_CLK(a.c0 / kPanel, 4);
   if (chosen) {                                        // T: the pivot rows' trackers only
     u32x4* wg = reinterpret_cast<u32x4*>(a.W + gi * kPanel);
     u32x4 o0, o1;
@@ -418,12 +463,12 @@ struct UpdArgs {
 // from an LDS copy (uniform addresses: broadcast reads).  Narrow spans keep >= 2 waves per SIMD
 // at n = 1024 (G = 1), which this latency-bound kernel needs.
 struct UpdSmem {
-  uint32_t perm_t[256][8];
+  LdsTab perm_t;
   uint32_t tT[16][kPanel * 8];             // per wave: T by step
 };
 
 __device__ __forceinline__ void update_task(const UpdArgs& a, uint32_t task, uint32_t lane, uint32_t* tT,
-                                            const uint32_t (*perm_t)[8])
+                                            const LdsTab& perm_t)
 {
   task = __builtin_amdgcn_readfirstlane(task);
   const uint32_t span = task % a.nspans;
@@ -463,8 +508,8 @@ __device__ __forceinline__ void update_task(const UpdArgs& a, uint32_t task, uin
 #pragma unroll
     for (int s = 0; s < static_cast<int>(kPanel); ++s) {
       const uint32_t c = (xw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
-      const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
-      const uint32_t t4 = perm_t[c][4];
+      const u32x4 tab = perm_t.a[c];
+      const uint32_t t4 = perm_t.b[c];
       acc_w ^= mul4(tab[0], tab[1], tab[2], tab[3], t4, tT[8 * s + d]);
     }
     if (((kw >> (8 * j)) & 0xFFu) == 0)
@@ -500,8 +545,8 @@ __device__ __forceinline__ void update_task(const UpdArgs& a, uint32_t task, uin
       for (int j = 0; j < kUpdRows; ++j) {
         const uint32_t wi = 8u * j + (t >> 2);
         const uint32_t c = (wv[wi] >> (8 * (t & 3))) & 0xFFu;   // 0: zero table
-        const u32x4 tab = *reinterpret_cast<const u32x4*>(&perm_t[c][0]);
-        const uint32_t t4 = perm_t[c][4];
+        const u32x4 tab = perm_t.a[c];
+        const uint32_t t4 = perm_t.b[c];
         acc[j] = __builtin_amdgcn_bitop3_b32(acc[j], __builtin_amdgcn_perm(tab[1], tab[0], sa),
                                              __builtin_amdgcn_perm(tab[3], tab[2], sb), 0x96) ^
                  __builtin_amdgcn_perm(t4, t4, se);
@@ -519,9 +564,9 @@ __device__ __forceinline__ void update_task(const UpdArgs& a, uint32_t task, uin
 
 __global__ __launch_bounds__(256) void dn_update(UpdArgs a)        // one task per wave
 {
-  __shared__ __attribute__((aligned(16))) uint32_t perm_t[256][8];
+  __shared__ __attribute__((aligned(16))) LdsTab perm_t;
   __shared__ __attribute__((aligned(16))) uint32_t tT_all[4][kPanel * 8];
-  for (uint32_t e = threadIdx.x; e < 256 * 8; e += 256) perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+  stage_tab(perm_t, dn_perm, threadIdx.x, 256);
   __syncthreads();
   update_task(a, blockIdx.x * 4u + (threadIdx.x >> 6), threadIdx.x & 63u, tT_all[threadIdx.x >> 6], perm_t);
 }
@@ -547,11 +592,17 @@ __global__ __launch_bounds__(1024) void dn_fused(FusedArgs f)
     panel_run<true>(f.pa, sm.p, blockIdx.x, threadIdx.x, blockDim.x);
     return;
   }
-  for (uint32_t e = threadIdx.x; e < 256 * 8; e += blockDim.x) sm.u.perm_t[e >> 3][e & 7] = dn_perm.w[e >> 3][e & 7];
+#ifdef NTC_DENSE_CLOCK
+  if (threadIdx.x == 0) atomicMin(&g_dn_clk[(f.pa.c0 / kPanel) * 8 + 6], wall_clock64());
+#endif
+  stage_tab(sm.u.perm_t, dn_perm, threadIdx.x, blockDim.x);
   __syncthreads();
   const uint32_t w = threadIdx.x >> 6;
-  if (w >= f.tpb) return;
-  update_task(f.ua, (blockIdx.x - f.nA) * f.tpb + w, threadIdx.x & 63u, sm.u.tT[w], sm.u.perm_t);
+  if (w < f.tpb) update_task(f.ua, (blockIdx.x - f.nA) * f.tpb + w, threadIdx.x & 63u, sm.u.tT[w], sm.u.perm_t);
+#ifdef NTC_DENSE_CLOCK
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&g_dn_clk[(f.pa.c0 / kPanel) * 8 + 7], wall_clock64());
+#endif
 }
 
 // inv[g][t][0..n) = X[g][piv[t]][np .. np + n)  (zeros for a singular generation)

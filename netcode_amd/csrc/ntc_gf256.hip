@@ -1642,8 +1642,17 @@ __device__ __forceinline__ void set_byte_dyn(uint32_t (&v)[W], uint32_t i, uint3
 // Gauss-Jordan step for column P (compile-time, so every register index is static): false when
 // column P has no nonzero at or below row P (M singular).  FM: m == 4 * W (every row word live),
 // so the per-word guards go away.
+// The plan's v_perm tables in LDS, split by dword so that per-lane gathers spread over the banks:
+// dwords 0-3 of c's table at a 16-byte pitch (ds_read_b128, 16 lanes per bank cycle: bank group c
+// mod 16), dword 4 at a 4-byte pitch (ds_read_b32, 32 lanes: bank c mod 32).  With the 8-dword
+// PermTables rows every b128 gather landed on c mod 8 and every fifth-dword gather on c mod 4.
+struct PlanTab {
+  uint4 a[256];
+  uint32_t b[256];
+};
+
 template <int W, int P, bool FM>
-__device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const uint32_t (*ptab)[8])
+__device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const PlanTab& ptab)
 {
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   constexpr int pw = P >> 2, ps = 8 * (P & 3);
@@ -1675,8 +1684,8 @@ __device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const ui
   const uint32_t* ti = d_pinv.w[piv];
   const uint32_t tinv[5] = {ti[0], ti[1], ti[2], ti[3], ti[4]};
   const uint32_t y = mul4(tinv, (col[pw] >> ps) & 0xFFu);    // A[P][c] / piv
-  const uint4 ab = *reinterpret_cast<const uint4*>(&ptab[y][0]);
-  const uint32_t ty[5] = {ab.x, ab.y, ab.z, ab.w, ptab[y][4]};
+  const uint4 ab = ptab.a[y];
+  const uint32_t ty[5] = {ab.x, ab.y, ab.z, ab.w, ptab.b[y]};
   F[pw] ^= 1u << ps;
 #pragma unroll
   for (int w = 0; w < W; ++w)
@@ -1685,7 +1694,7 @@ __device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const ui
 }
 
 template <int W, int P, int RM, bool FM>
-__device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], uint32_t m, const uint32_t (*ptab)[8])
+__device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], uint32_t m, const PlanTab& ptab)
 {
   if constexpr (P == RM) {
     return true;
@@ -1724,15 +1733,14 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   DBG_CLK(0);
   static_assert(RM == 8 || RM == 16 || RM == 32, "the column layout needs 2 * RM <= 64 lanes");
   constexpr int W = RM / 4;
-  __shared__ __attribute__((aligned(16))) uint32_t ptab[256][8];
+  __shared__ __attribute__((aligned(16))) PlanTab ptab;
   __shared__ uint16_t s_miss[kPlanWaves][RM];
   __shared__ uint16_t s_recv[kPlanWaves][RM];
   // scratch of the rank screening: received rows x (W + 1) dwords
   __shared__ __attribute__((aligned(16))) uint32_t s_scr[kPlanWaves][RM * (W + 1)];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(&d_perm.w[0][0]);
-    uint4* dst = reinterpret_cast<uint4*>(&ptab[0][0]);
-    for (uint32_t i = threadIdx.x; i < 512u; i += 64u * kPlanWaves) dst[i] = src[i];
+  for (uint32_t c = threadIdx.x; c < 256u; c += 64u * kPlanWaves) {
+    ptab.a[c] = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);
+    ptab.b[c] = d_perm.w[c][4];
   }
   __syncthreads();   // the only block-wide barrier: the waves below are independent generations
   const uint32_t lane = threadIdx.x & 63u;
@@ -1748,8 +1756,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   auto tab = [&](uint32_t c, uint32_t (&t)[5]) {
-    const uint4 ab = *reinterpret_cast<const uint4*>(&ptab[c][0]);
-    t[0] = ab.x; t[1] = ab.y; t[2] = ab.z; t[3] = ab.w; t[4] = ptab[c][4];
+    const uint4 ab = ptab.a[c];
+    t[0] = ab.x; t[1] = ab.y; t[2] = ab.z; t[3] = ab.w; t[4] = ptab.b[c];
   };
 
   const uint32_t k = a.k, r = a.r;

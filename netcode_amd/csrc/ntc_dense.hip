@@ -163,8 +163,6 @@ struct PanelSmem {
   // panel's columns, with their v_perm selectors; partial products of the cooperative pass
   u32x4 tsel[kPanel][8];
   u32x4 psel[kPanel][8];
-  uint32_t part[2][8][64];
-  uint32_t part2[2][8][64];
   uint32_t stopv[2];                       // owner's stop step per phase
   uint32_t cm[2];                          // election masks per phase
   uint32_t ne[16];                         // wave has eligible rows
@@ -184,9 +182,11 @@ struct PanelSmem {
 // from the pre-update matrix -- W_i = X_i[prev panel] * T, then X_i[panel] ^= sum_t W_i[t] *
 // X[piv_t][panel], the update's own arithmetic, split over all waves -- and the other waves derive
 // their own rows only if the owner does not finish the panel alone (an election).
+// LOOKAHEAD: part = dynamic LDS of (nw + 1) x 8 x 64 dwords (per wave: partial words of the
+// owner rows, then their XOR over the waves)
 template <bool LOOKAHEAD>
 __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uint32_t g, uint32_t i,
-                                          uint32_t nthreads)
+                                          uint32_t nthreads, uint32_t* part = nullptr)
 {
   const uint32_t lane = i & 63u, w = i >> 6, nw = nthreads >> 6;
   const uint32_t np = a.np, P = 2 * np;
@@ -231,8 +231,9 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       v[4] = q1[0]; v[5] = q1[1]; v[6] = q1[2]; v[7] = q1[3];
     }
   } else {
-    // the owner's 64 rows, all waves: job (d, h) = word d of W_i (phase 1) and of the panel
-    // columns (phase 2) over the 16 terms of half h
+    // the owner's 64 rows, all waves: wave w takes the terms s = w, w + nw, ... of W_i (phase 1)
+    // and then of the panel columns (phase 2), all 8 words each -- every table is gathered once
+    // per lane -- and the words are XOR-reduced over the waves' partials in LDS
     const uint32_t orow = owner * 64u + lane;
     const bool orow_ok = orow < np;
     const size_t go = static_cast<size_t>(g) * np + (orow_ok ? orow : 0u);
@@ -242,40 +243,54 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       own0 = src[0];
       own1 = src[1];
     }
-    for (uint32_t job = w; job < 16; job += nw) {
-      const uint32_t d = job & 7u, h = job >> 3;
-      u32x4 x4 = {0, 0, 0, 0};
-      if (orow_ok) x4 = *reinterpret_cast<const u32x4*>(a.X + go * P + cp + 16u * h);
-      uint32_t acc = 0;
+    // part: region A = [nw][8][64] partial words, region B = [8][64] reduced words
+    uint32_t* pa = part;
+    uint32_t* pb = part + nw * 8u * 64u;
+    // XOR of the nw partials of word d, written to B (waves share the 8 words)
+    auto reduce_words = [&]() {
+      for (uint32_t d = w; d < 8; d += nw) {
+        uint32_t y = 0;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const uint32_t b = (x4[s >> 2] >> (8 * (s & 3))) & 0xFFu;
-        const u32x4 tf = sm.perm_t.a[b];
-        acc ^= mul_sel(tf, sm.perm_t.b[b], sm.tsel[16u * h + s][d]);
+        for (uint32_t u = 0; u < 16; ++u)
+          if (u < nw) y ^= pa[(u * 8u + d) * 64u + lane];
+        pb[d * 64u + lane] = y;
       }
-      sm.part[h][d][lane] = acc;
+    };
+    {
+      uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t s = w; s < kPanel; s += nw) {
+        const uint32_t xq = orow_ok ? *reinterpret_cast<const uint32_t*>(a.X + go * P + cp + (s & ~3u)) : 0u;
+        const uint32_t b = (xq >> (8 * (s & 3))) & 0xFFu;
+        const u32x4 tf = sm.perm_t.a[b];
+        const uint32_t tf4 = sm.perm_t.b[b];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.tsel[s][d]);
+      }
+#pragma unroll
+      for (int d = 0; d < 8; ++d) pa[(w * 8u + d) * 64u + lane] = acc[d];
     }
     __syncthreads();
-    for (uint32_t job = w; job < 16; job += nw) {
-      const uint32_t d = job & 7u, h = job >> 3;
-      uint32_t acc = 0;
+    reduce_words();                                      // B = W_i
+    __syncthreads();
+    {
+      uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t t = w; t < kPanel; t += nw) {
+        const uint32_t b = (pb[(t >> 2) * 64u + lane] >> (8 * (t & 3))) & 0xFFu;
+        const u32x4 tf = sm.perm_t.a[b];
+        const uint32_t tf4 = sm.perm_t.b[b];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t wd = sm.part[0][4u * h + q][lane] ^ sm.part[1][4u * h + q][lane];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t b = (wd >> (8 * k)) & 0xFFu;
-          const u32x4 tf = sm.perm_t.a[b];
-          acc ^= mul_sel(tf, sm.perm_t.b[b], sm.psel[16u * h + 4 * q + k][d]);
-        }
+        for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.psel[t][d]);
       }
-      sm.part2[h][d][lane] = acc;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) pa[(w * 8u + d) * 64u + lane] = acc[d];
     }
+    __syncthreads();
+    reduce_words();                                      // B = sum_t W_i[t] X[piv_t][panel]
     __syncthreads();
     if (w == owner) {
       const uint32_t x8[8] = {own0[0], own0[1], own0[2], own0[3], own1[0], own1[1], own1[2], own1[3]};
 #pragma unroll
-      for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ sm.part2[0][d][lane] ^ sm.part2[1][d][lane] : 0u;
+      for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ pb[d * 64u + lane] : 0u;
       have = true;
     }
     if (g == 0) DN_CLK(a.c0 / kPanel, 2);
@@ -589,7 +604,8 @@ __global__ __launch_bounds__(1024) void dn_fused(FusedArgs f)
     UpdSmem u;
   } sm;
   if (blockIdx.x < f.nA) {
-    panel_run<true>(f.pa, sm.p, blockIdx.x, threadIdx.x, blockDim.x);
+    extern __shared__ __attribute__((aligned(16))) uint32_t dn_part[];
+    panel_run<true>(f.pa, sm.p, blockIdx.x, threadIdx.x, blockDim.x, dn_part);
     return;
   }
 #ifdef NTC_DENSE_CLOCK
@@ -713,7 +729,12 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
       const uint64_t spread = G < 240 ? 240 - G : 16;
       fa.tpb = static_cast<uint32_t>(std::min<uint64_t>(nw, std::max<uint64_t>(1, (waves + spread - 1) / spread)));
       const uint64_t nb = (waves + fa.tpb - 1) / fa.tpb;
-      hipLaunchKernelGGL(dn_fused, dim3(static_cast<uint32_t>(G + nb)), dim3(threads), 0, st, fa);
+      const size_t part_bytes = static_cast<size_t>(nw + 1) * 8 * 64 * 4;
+      static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(dn_fused),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   static_cast<int>(17 * 8 * 64 * 4)) == hipSuccess;
+      (void)attr;
+      hipLaunchKernelGGL(dn_fused, dim3(static_cast<uint32_t>(G + nb)), dim3(threads), part_bytes, st, fa);
       if ((rc = hip_check(hipGetLastError(), "dn_fused launch"))) return rc;
     } else {
       hipLaunchKernelGGL(dn_update, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(256), 0, st, ua);

@@ -1639,9 +1639,21 @@ __device__ __forceinline__ void set_byte_dyn(uint32_t (&v)[W], uint32_t i, uint3
   }
 }
 
-// Gauss-Jordan step for column P (compile-time, so every register index is static): false when
-// column P has no nonzero at or below row P (M singular).  FM: m == 4 * W (every row word live),
-// so the per-word guards go away.
+// The same for a wave-uniform i: one indexed register move (s_set_gpr_idx) instead of a select
+// per word, whose 64-bit lane masks were the plan's SGPR spills.
+template <int W>
+__device__ __forceinline__ uint32_t byte_dyn_u(const uint32_t (&v)[W], uint32_t i)
+{
+  return (v[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+}
+
+template <int W>
+__device__ __forceinline__ void set_byte_dyn_u(uint32_t (&v)[W], uint32_t i, uint32_t b)
+{
+  const uint32_t sh = 8u * (i & 3u);
+  v[i >> 2] = (v[i >> 2] & ~(0xFFu << sh)) | ((b & 0xFFu) << sh);
+}
+
 // The plan's v_perm tables in LDS, split by dword so that per-lane gathers spread over the banks:
 // dwords 0-3 of c's table at a 16-byte pitch (ds_read_b128, 16 lanes per bank cycle: bank group c
 // mod 16), dword 4 at a 4-byte pitch (ds_read_b32, 32 lanes: bank c mod 32).  With the 8-dword
@@ -1651,8 +1663,10 @@ struct PlanTab {
   uint32_t b[256];
 };
 
-template <int W, int P, bool FM>
-__device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const PlanTab& ptab)
+// Gauss-Jordan step for column P (compile-time, so every register index is static): false when
+// column P has no nonzero at or below row P (M singular).
+template <int W, int P>
+__device__ __forceinline__ bool gj_step(uint32_t (&col)[W], const PlanTab& ptab)
 {
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   constexpr int pw = P >> 2, ps = 8 * (P & 3);
@@ -1674,9 +1688,9 @@ __device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const Pl
       if (q == kNone && nz != 0) q = 4u * w + (__builtin_ctz(nz) >> 3);
     }
     if (q == kNone) return false;
-    const uint32_t bp = (col[pw] >> ps) & 0xFFu, bq = byte_dyn<W>(col, q);
+    const uint32_t bp = (col[pw] >> ps) & 0xFFu, bq = byte_dyn_u<W>(col, q);
     col[pw] = (col[pw] & ~(0xFFu << ps)) | (bq << ps);
-    set_byte_dyn<W>(col, q, bp);
+    set_byte_dyn_u<W>(col, q, bp);
 #pragma unroll
     for (int w = 0; w < W; ++w) F[w] = __builtin_amdgcn_readlane(col[w], P);
     piv = (F[pw] >> ps) & 0xFFu;
@@ -1689,19 +1703,18 @@ __device__ __forceinline__ bool gj_step(uint32_t (&col)[W], uint32_t m, const Pl
   F[pw] ^= 1u << ps;
 #pragma unroll
   for (int w = 0; w < W; ++w)
-    if (FM || 4u * w < m) col[w] ^= mul4(ty, F[w]);
+    col[w] ^= mul4(ty, F[w]);
   return true;
 }
 
-template <int W, int P, int RM, bool FM>
-__device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], uint32_t m, const PlanTab& ptab)
+template <int W, int P, int RM>
+__device__ __forceinline__ bool gj_pivots(uint32_t (&col)[W], const PlanTab& ptab)
 {
   if constexpr (P == RM) {
     return true;
   } else {
-    if (!FM && static_cast<uint32_t>(P) >= m) return true;
-    if (!gj_step<W, P, FM>(col, m, ptab)) return false;
-    return gj_pivots<W, P + 1, RM, FM>(col, m, ptab);
+    if (!gj_step<W, P>(col, ptab)) return false;
+    return gj_pivots<W, P + 1, RM>(col, ptab);
   }
 }
 
@@ -1823,6 +1836,18 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
     };
     // rows 0 .. m-2: the first m-1 received repairs; identity block in lanes m .. 2m-1
     uint32_t orig[W];
+    // Columns (lanes) m .. RM-1 pad M to RM x RM with an identity block, so the Gauss-Jordan
+    // always runs all RM pivots, with no per-m branch or per-word guard (block-diagonal: M^-1 is
+    // unchanged, rows >= m stay zero in every other column); the augmented identity of the m
+    // chosen repairs sits in lanes RM .. RM+m-1.  Lane indices come from opaque copies: compared
+    // directly, their lane masks were shared with the emit phase's and stayed live across the
+    // unrolled Gauss-Jordan as SGPR spills.
+    uint32_t idl = lane - RM;
+    asm volatile("" : "+v"(idl));
+    uint32_t pdl = lane;
+    asm volatile("" : "+v"(pdl));
+    const uint32_t idr = idl < m ? idl : (pdl >= m && pdl < static_cast<uint32_t>(RM) ? pdl : ~0u);
+    const uint32_t idb = idr != ~0u ? (1u << (8u * (idr & 3u))) : 0u, idw = idr >> 2;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       uint32_t v = 0;
@@ -1831,9 +1856,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         const uint32_t q = 4u * w + b;
         if (q + 1 < m) v |= coef(__builtin_amdgcn_readlane(rid1, q)) << (8 * b);
       }
-      if (lane >= m && lane < 2 * m && ((lane - m) >> 2) == static_cast<uint32_t>(w))
-        v |= 1u << (8u * ((lane - m) & 3u));
-      orig[w] = v;
+      orig[w] = v | (idw == static_cast<uint32_t>(w) ? idb : 0u);
     }
     // After a singular first candidate: rank screening instead of one Gauss-Jordan per further
     // candidate (decoder.cc:448-468 tries t = m, m+1, ... in turn).  {first m-1 repairs} + {t} is
@@ -1903,14 +1926,23 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
     bool ok = false;
     uint32_t t = m - 1;
     DBG_CLK(1);
-    for (; t < nrecv; ++t) {
-      // row m-1: received repair t (decoder.cc:448-468 retries with each newer repair)
-      const uint32_t ct = coef(__builtin_amdgcn_readlane(rid1, t));
+    // row m-1's byte of each word as a VGPR mask, made once: a uniform select per word here
+    // became 64-bit lane masks that stayed live across the unrolled Gauss-Jordan (SGPR spills)
+    const uint32_t shm = 8u * ((m - 1) & 3u);
+    uint32_t selm[W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) col[w] = orig[w];
-      set_byte_dyn<W>(col, m - 1, ct | byte_dyn<W>(orig, m - 1));
-      if (m == static_cast<uint32_t>(RM) ? gj_pivots<W, 0, RM, true>(col, m, ptab)
-                                         : gj_pivots<W, 0, RM, false>(col, m, ptab)) {
+    for (int w = 0; w < W; ++w) {
+      uint32_t s_ = static_cast<uint32_t>(w) == ((m - 1) >> 2) ? ~0u : 0u;
+      asm volatile("" : "+v"(s_));
+      selm[w] = s_;
+    }
+    for (; t < nrecv; ++t) {
+      // row m-1: received repair t (decoder.cc:448-468 retries with each newer repair); the
+      // row holds only its identity bit in orig
+      const uint32_t ct = coef(__builtin_amdgcn_readlane(rid1, t)) << shm;
+#pragma unroll
+      for (int w = 0; w < W; ++w) col[w] = orig[w] | (ct & selm[w]);
+      if (gj_pivots<W, 0, RM>(col, ptab)) {
         ok = true;
         break;
       }
@@ -1944,9 +1976,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         for (int w = 0; w < W; ++w)
           if (4u * w < rp) d[w] = v[w];
       };
-      // the rest in two versions: FM (m == RM: every row word live, no per-word guards) or not
-      auto emit_phase = [&](auto fm_c) {
-      constexpr bool FM = decltype(fm_c)::value;
+      {   // every row word is computed: the words of rows >= m are zero (no per-word guards)
       uint32_t LO[W], HI[W];     // this lane's decoded-size terms, low and high length bytes
 #pragma unroll
       for (int w = 0; w < W; ++w) LO[w] = HI[w] = 0;
@@ -1955,8 +1985,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         tab(len & 0xFFu, tl);
         tab(len >> 8, th);
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (FM || 4u * w < m) {
+        for (int w = 0; w < W; ++w) {
             const uint32_t s0 = v[w] & 0x07070707u, s1 = (v[w] >> 3) & 0x07070707u;
             const uint32_t s2 = (v[w] >> 6) & 0x03030303u;
             LO[w] ^= xor3(__builtin_amdgcn_perm(tl[1], tl[0], s0), __builtin_amdgcn_perm(tl[3], tl[2], s1),
@@ -1981,11 +2010,11 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       const uint32_t row_r1 = (lane == m - 1) ? t_rid1 : rid1;
       // Positions 0 .. m-1: the chosen repairs, D[s][q] = Minv[s][q] = column m + q; the size of
       // each lane's repair from the preloaded sizes (shuffled with every lane active)
-      const bool rep_lane = lane >= m && lane < 2 * m;
-      const uint32_t rq_l = rep_lane ? ((lane - m + 1 < m) ? recv[lane - m] : recv[t]) : 0u;
+      const bool rep_lane = lane >= static_cast<uint32_t>(RM) && lane < RM + m;
+      const uint32_t rq_l = rep_lane ? ((lane - RM + 1 < m) ? recv[lane - RM] : recv[t]) : 0u;
       const uint32_t rsz_l = __shfl(rsv, rq_l);
       if (rep_lane) {
-        const uint32_t q = lane - m;
+        const uint32_t q = lane - RM;
         const uint32_t rq = rq_l;
         pin[q] = static_cast<uint16_t>(k + rq);
         put_row(q, NTC_PLAN_ARG(rows_rep) + (static_cast<uint64_t>(g) * r + rq) * NTC_PLAN_ARG(rows_stride));
@@ -2028,8 +2057,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             uint32_t sq[3][W];
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-              if (!(FM || 4u * w < m)) continue;
-              const uint32_t cw = __builtin_amdgcn_readlane(col[w], m + q);
+              const uint32_t cw = __builtin_amdgcn_readlane(col[w], RM + q);
               sq[0][w] = cw & 0x07070707u;
               sq[1][w] = (cw >> 3) & 0x07070707u;
               sq[2][w] = (cw >> 6) & 0x03030303u;
@@ -2040,8 +2068,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             }
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              if (FM || 4u * w < m)
-                acc[w] ^= xor3(__builtin_amdgcn_perm(tc[1], tc[0], sq[0][w]),
+              acc[w] ^= xor3(__builtin_amdgcn_perm(tc[1], tc[0], sq[0][w]),
                                __builtin_amdgcn_perm(tc[3], tc[2], sq[1][w]),
                                __builtin_amdgcn_perm(tc[4], tc[4], sq[2][w]));
           }
@@ -2054,8 +2081,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (FM || 4u * w < m) {
+        for (int w = 0; w < W; ++w) {
             LO[w] ^= __shfl_xor(LO[w], off);
             HI[w] ^= __shfl_xor(HI[w], off);
           }
@@ -2063,9 +2089,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
         const uint32_t lo = byte_dyn<W>(LO, lane), hi = byte_dyn<W>(HI, lane);
         slen[miss[lane]] = static_cast<uint16_t>(lo | (hi << 8));
       }
-      };
-      if (m == static_cast<uint32_t>(RM)) emit_phase(std::true_type{});
-      else emit_phase(std::false_type{});
+      }
     }
   }
   if (lane == 0) {

@@ -84,7 +84,7 @@ def parse():
     pp.add_argument("--rate", type=int, default=4)
     pp.add_argument("--loss", type=float, default=0.1)
     pp.add_argument("--c-items", type=int, default=128, help="items per flow of the C-level legs")
-    pp.add_argument("--pp-reps", type=int, default=3, help="interleaved runs of each C-level leg (best kept)")
+    pp.add_argument("--pp-reps", type=int, default=5, help="interleaved runs of each C-level leg (best kept)")
     return p.parse_args()
 
 

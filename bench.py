@@ -640,7 +640,11 @@ def host_rate_wire(w, reps=3):
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
     rate = G * k * w.S / min(times[1:]) / 2**30
-    ok = torch.equal(h_rep_pkts, rpk_dev.cpu()) and torch.equal(h_rep_len, rlen_dev.cpu())
+    # each packet's bytes up to its length (the slot bytes past it are not part of the packet)
+    d_pk, d_len = rpk_dev.cpu(), rlen_dev.cpu()
+    inpkt = torch.arange(rps)[None, :] < d_len.to(torch.int64)[:, None]
+    checks = {"packet_lengths": torch.equal(h_rep_len, d_len),
+              "packet_bytes": torch.equal(h_rep_pkts[inpkt], d_pk[inpkt])}
     from netcode_amd import status_to_numpy
     st = status_to_numpy(h_st)
     lost = (w.smask == 0).cpu()
@@ -648,9 +652,10 @@ def host_rate_wire(w, reps=3):
     rec_gen = torch.repeat_interleave(torch.arange(G), lost.sum(1))   # generation of each lost row
     src_lost = w.src.cpu()[lost]
     sel = dec[rec_gen]
-    ok = ok and torch.equal(h_rec[sel], src_lost[sel])
-    ok = ok and torch.equal(h_dec_len[lost][sel], w.src_len.cpu()[lost][sel])
-    return rate, bool(ok), h_rep_pkts, h_rep_len
+    checks["recovered_rows"] = torch.equal(h_rec[sel], src_lost[sel])
+    checks["recovered_lengths"] = torch.equal(h_dec_len[lost][sel], w.src_len.cpu()[lost][sel])
+    host_rate_wire.checks = checks
+    return rate, all(checks.values()), h_rep_pkts, h_rep_len
 
 
 def oracle_check(smp, threads):
@@ -971,6 +976,8 @@ def main():
             "received source packets + repair packets H2D -> read_packets -> decode -> lost rows "
             "packed D2H; 3 streams, chunks of G/16")
         line["host_resident_wire_bit_exact"] = hwok
+        if not hwok:
+            line["host_resident_wire_checks"] = host_rate_wire.checks
         good = good and hwok
         if smp is not None:
             gi = torch.from_numpy(smp["g"])

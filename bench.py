@@ -846,8 +846,19 @@ def main():
         step = graph.replay
     engine.timing_log(nprof * 16)        # the log's events exist before the clock starts ...
     engine.timing_kinds(())              # ... but nothing is logged until the profiled steps
-    for _ in range(a.warmup):
+    # Warmup: the W steps asked for, continued (synchronised) until the device has run this load
+    # for at least NTC_BENCH_MIN_WARMUP_MS (default 60): from a cold start the MI355X's clocks take
+    # ~12 config-3 steps (~25 ms) to reach their steady step time (3.3 -> 1.85 ms,
+    # tools/step_times.py, profiles/r04/final/step_times.txt), so at --warmup 5 a quarter of a
+    # 20-step timed region would still be ramping.  The line reports both counts.
+    min_warm = float(os.environ.get("NTC_BENCH_MIN_WARMUP_MS", "60")) / 1e3
+    t_warm = time.perf_counter()
+    warm_run = 0
+    while warm_run < a.warmup or (time.perf_counter() - t_warm < min_warm and warm_run < 1000):
         step()
+        warm_run += 1
+        if warm_run >= a.warmup:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
 
     def barrier():
@@ -933,7 +944,7 @@ def main():
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": n_gpus, "ranks": world,
             "rank_sync": backend if world > 1 else None,
             "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "warmup": a.warmup, "warmup_steps_run": warm_run, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8 (GF(2^8))",
             "data": "synthetic (seeded random payloads, exact-m uniform loss)",
             "config": {"workload": a.config, "k": k, "r": r, "S": S, "stride": stride,

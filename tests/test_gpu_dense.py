@@ -43,6 +43,22 @@ def test_dense_invert(gpu, oracle, n):
         assert (inv[g] == o_inv).all(), (n, g)
 
 
+def test_dense_invert_many_generations(gpu, oracle):
+    """Many generations per launch: the lookahead launches (dn_fused) run one panel block per
+    generation ahead of the update blocks; two singular generations among them."""
+    import torch
+    from netcode_amd import DenseCode
+    G, n = 40, 96
+    mats = _mats(G, n, seed=11, singular=(7, 31))
+    inv, ok = DenseCode(gpu).invert(_dev(mats, gpu))
+    torch.cuda.synchronize(gpu)
+    inv, ok = inv.cpu().numpy(), ok.cpu().numpy()
+    for g in range(G):
+        o_ok, _, o_inv = oracle.dense_decode(mats[g], np.zeros((n, 16), np.uint8))
+        assert bool(ok[g]) == o_ok, g
+        assert (inv[g] == o_inv).all(), g
+
+
 def test_dense_invert_structured(gpu, oracle):
     """Zero pivots that force row exchanges, identity, permutation, all-zero matrices."""
     import torch

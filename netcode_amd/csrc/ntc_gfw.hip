@@ -5,11 +5,13 @@
 // (w=16), x^32 + 0x400007 (w=32).  Region semantics of multiply_region.w32: w=4 multiplies every
 // nibble, w=8 every byte, w=16 / w=32 every little-endian 16- / 32-bit word of the region.
 //
-// Device work is a shift-and-add multiply on packed elements: a dword holds 8 / 4 / 2 / 1
-// elements, xtime (multiply by alpha) is a masked shift plus a reduction constant for all of them
-// at once, and the wave-uniform coefficient's bits select which powers are accumulated -- at most
-// w xtime steps per dword and input, no tables.  This serves the per-packet C ABI (libntc.so) for
-// w != 8 and the batched combine for any w; the GF(2^8) batch path keeps its dedicated kernels
+// Device work is shift-and-add on packed elements: a dword holds 8 / 4 / 2 / 1 elements and xtime
+// (multiply by alpha) is a shift plus a reduction constant for all of them at once (packed 16-bit
+// shifts for w = 16, an arithmetic-shift mask for w = 32).  The batched combine walks the powers
+// x * alpha^t once per input dword and adds each into the rows whose coefficient has bit t set --
+// a wave-uniform 0 / -1 mask per (row, t), so one AND-XOR per (row, t, dword) -- which amortises
+// the w xtime steps over up to 8 rows.  This serves the per-packet C ABI (libntc.so) for w != 8
+// and the batched combine for any w; the GF(2^8) batch path keeps its dedicated kernels
 // (ntc_gf256.hip).  Host-side scalar arithmetic (coefficient, multiply, invert, multiply_size) is
 // the carry-less product reduced by the same polynomials.
 #include <hip/hip_runtime.h>
@@ -22,15 +24,13 @@
 namespace ntcgpu {
 namespace {
 
+// byte-packed fields (w = 4, 8): per-element shift mask, the elements' top bits, shift to bit 0
 template <int W> struct Packed;
 template <> struct Packed<4> {
-  static constexpr uint32_t keep = 0xEEEEEEEEu, top = 0x11111111u, red = 0x3u, shift = 3;
+  static constexpr uint32_t keep = 0xEEEEEEEEu, top = 0x11111111u, shift = 3;
 };
 template <> struct Packed<8> {
-  static constexpr uint32_t keep = 0xFEFEFEFEu, top = 0x01010101u, red = 0x1Du, shift = 7;
-};
-template <> struct Packed<16> {
-  static constexpr uint32_t keep = 0xFFFEFFFEu, top = 0x00010001u, red = 0x100Bu, shift = 15;
+  static constexpr uint32_t keep = 0xFEFEFEFEu, top = 0x01010101u, shift = 7;
 };
 
 // alpha * x for every element packed in x
@@ -38,9 +38,26 @@ template <int W>
 __device__ __forceinline__ uint32_t xtime(uint32_t y)
 {
   if constexpr (W == 32) {
-    return (y << 1) ^ ((0u - (y >> 31)) & 0x00400007u);
+    return (y << 1) ^ (static_cast<uint32_t>(static_cast<int32_t>(y) >> 31) & 0x00400007u);
+  } else if constexpr (W == 16) {
+    // two u16 lanes: per-half shift (no carry across) and per-half sign mask
+    typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 h = __builtin_bit_cast(u16x2, y);
+    const u16x2 sh = h << static_cast<uint16_t>(1);
+    const i16x2 sg = __builtin_bit_cast(i16x2, y) >> static_cast<int16_t>(15);
+    return __builtin_bit_cast(uint32_t, sh) ^ (__builtin_bit_cast(uint32_t, sg) & 0x100B100Bu);
   } else {
-    return ((y << 1) & Packed<W>::keep) ^ (((y >> Packed<W>::shift) & Packed<W>::top) * Packed<W>::red);
+    const uint32_t t = (y >> Packed<W>::shift) & Packed<W>::top;
+    uint32_t red;
+    if constexpr (W == 4) {
+      red = t | (t << 1);                                                      // * 0x3
+    } else {                                                                   // * 0x1D, per u16 half
+      typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+      const u16x2 k = {0x1D, 0x1D};
+      red = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, t) * k);
+    }
+    return ((y << 1) & Packed<W>::keep) ^ red;
   }
 }
 
@@ -65,30 +82,67 @@ struct CombineArgs {
   uint8_t* out;            // [G][rows][stride]
 };
 
-// One thread per 16-byte column chunk of one output row.
-template <int W>
-__global__ __launch_bounds__(256) void gfw_combine(CombineArgs a)
+// One wave per (generation, 1 KiB column span, group of RB rows); a lane owns 16 bytes of the span
+// for all RB rows.  Per input: the 4 dwords walk x, x*alpha, ..., x*alpha^(W-1) and every row adds
+// the powers its coefficient selects (mask 0 / -1 from bit t of the wave-uniform coefficient).
+// The next input's 16 bytes are loaded before this one's powers are walked.
+constexpr uint32_t kGfwSpan = 1024;
+
+template <int W, int RB>
+__global__ __launch_bounds__(256) void gfw_combine(CombineArgs a, uint32_t nspan, uint32_t ngrp)
 {
-  const uint32_t chunks = a.stride / 16u;
-  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  const uint64_t per_g = static_cast<uint64_t>(a.rows) * chunks;
-  if (t >= per_g * a.G) return;
-  const uint32_t g = static_cast<uint32_t>(t / per_g);
-  const uint32_t rem = static_cast<uint32_t>(t % per_g);
-  const uint32_t j = rem / chunks, col = 16u * (rem % chunks);
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  const uint8_t* in = a.in + static_cast<size_t>(g) * a.k * a.stride + col;
-  const uint32_t* cf = a.coef + static_cast<size_t>(g) * a.k * a.rows + j;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t per_g = nspan * ngrp;
+  if (wave >= a.G * per_g) return;
+  const uint32_t g = wave / per_g, rem = wave % per_g;
+  const uint32_t span = rem % nspan, r0 = (rem / nspan) * RB;
+  const uint32_t col = span * kGfwSpan + 16u * lane;
+  const bool act = col < a.stride;
+  const uint32_t nr = a.rows - r0 < static_cast<uint32_t>(RB) ? a.rows - r0 : static_cast<uint32_t>(RB);
+  const uint8_t* in = a.in + static_cast<size_t>(g) * a.k * a.stride + (act ? col : 0u);
+  const uint32_t* cf = a.coef + static_cast<size_t>(g) * a.k * a.rows + r0;
+  uint32_t acc[RB][4];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[r][d] = 0;
+  uint4 nx = act ? *reinterpret_cast<const uint4*>(in) : make_uint4(0, 0, 0, 0);
   for (uint32_t i = 0; i < a.k; ++i) {
-    const uint32_t c = cf[static_cast<size_t>(i) * a.rows];   // per lane: a wave spans rows
-    if (c == 0) continue;
-    const uint4 x = *reinterpret_cast<const uint4*>(in + static_cast<size_t>(i) * a.stride);
-    acc.x ^= mulw<W>(c, x.x);
-    acc.y ^= mulw<W>(c, x.y);
-    acc.z ^= mulw<W>(c, x.z);
-    acc.w ^= mulw<W>(c, x.w);
+    uint32_t y[4] = {nx.x, nx.y, nx.z, nx.w};
+    if (act && i + 1 < a.k) nx = *reinterpret_cast<const uint4*>(in + static_cast<size_t>(i + 1) * a.stride);
+    uint32_t c[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+      c[r] = static_cast<uint32_t>(r) < nr ? __builtin_amdgcn_readfirstlane(cf[static_cast<size_t>(i) * a.rows + r]) : 0u;
+    if constexpr (W < 32) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) c[r] &= (1u << W) - 1u;
+    }
+    uint32_t any = 0;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) any |= c[r];
+    if (any == 0) continue;                             // wave-uniform
+#pragma unroll
+    for (int t = 0; t < W; ++t) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const uint32_t m = 0u - ((c[r] >> t) & 1u);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[r][d] = __builtin_amdgcn_bitop3_b32(acc[r][d], y[d], m, 0x78);   // a ^ (y & m)
+      }
+      if (t + 1 < W) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) y[d] = xtime<W>(y[d]);
+      }
+    }
   }
-  *reinterpret_cast<uint4*>(a.out + (static_cast<size_t>(g) * a.rows + j) * a.stride + col) = acc;
+  if (!act) return;
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+    if (static_cast<uint32_t>(r) < nr)
+      *reinterpret_cast<uint4*>(a.out + (static_cast<size_t>(g) * a.rows + r0 + r) * a.stride + col) =
+          make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
 // dst[0..len) = c * src (+ dst); word boundaries relative to the region start; a partial last word
@@ -178,14 +232,27 @@ int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k
   if (!valid_w(w)) return fail(NTC_GPU_EINVAL, "w must be 4, 8, 16 or 32");
   if (G == 0 || k == 0 || rows == 0) return fail(NTC_GPU_EINVAL, "G, k and rows must be > 0");
   if (stride == 0 || stride % 16 != 0) return fail(NTC_GPU_EINVAL, "stride must be a non-zero multiple of 16");
-  const uint64_t threads = static_cast<uint64_t>(G) * rows * (stride / 16u);
-  const uint64_t blocks = (threads + 255) / 256;
-  if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
+  // rows per wave: 8, or the next power of two covering fewer rows
+  const uint32_t rb = rows >= 8 ? 8 : rows > 2 ? 4 : rows;
+  const uint32_t nspan = (stride + kGfwSpan - 1) / kGfwSpan, ngrp = (rows + rb - 1) / rb;
+  const uint64_t waves = static_cast<uint64_t>(G) * nspan * ngrp;
+  const uint64_t blocks = (waves + 3) / 4;
+  if (blocks > 0x7FFFFFFFull || waves > 0xFFFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   (void)hipSetDevice(e->device);
   CombineArgs a{G, k, rows, stride, in, coef, out};
-  auto* fn = w == 4 ? gfw_combine<4> : w == 8 ? gfw_combine<8> : w == 16 ? gfw_combine<16> : gfw_combine<32>;
+  using Fn = void (*)(CombineArgs, uint32_t, uint32_t);
+  Fn fn;
+  switch (w * 16 + rb) {
+#define NTC_GFW_CASE(W_, RB_) case W_ * 16 + RB_: fn = gfw_combine<W_, RB_>; break;
+    NTC_GFW_CASE(4, 1) NTC_GFW_CASE(4, 2) NTC_GFW_CASE(4, 4) NTC_GFW_CASE(4, 8)
+    NTC_GFW_CASE(8, 1) NTC_GFW_CASE(8, 2) NTC_GFW_CASE(8, 4) NTC_GFW_CASE(8, 8)
+    NTC_GFW_CASE(16, 1) NTC_GFW_CASE(16, 2) NTC_GFW_CASE(16, 4) NTC_GFW_CASE(16, 8)
+    NTC_GFW_CASE(32, 1) NTC_GFW_CASE(32, 2) NTC_GFW_CASE(32, 4) NTC_GFW_CASE(32, 8)
+#undef NTC_GFW_CASE
+    default: return fail(NTC_GPU_EINVAL, "w must be 4, 8, 16 or 32");
+  }
   hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), a);
+                     static_cast<hipStream_t>(stream), a, nspan, ngrp);
   return hip_check(hipGetLastError(), "gfw_combine launch");
 }
 

@@ -33,7 +33,9 @@ def test_region_multiply(gpu, oracle, w):
 
 
 @pytest.mark.parametrize("w", WS)
-@pytest.mark.parametrize("G,k,rows,stride", [(3, 5, 2, 64), (2, 17, 4, 1504), (1, 1, 1, 16)])
+# row groups of 8 / 4 / 2 / 1 per wave, 1 KiB column spans (ragged last span), all-zero sources
+@pytest.mark.parametrize("G,k,rows,stride", [(3, 5, 2, 64), (2, 17, 4, 1504), (1, 1, 1, 16), (2, 6, 9, 2064),
+                                             (1, 3, 8, 1024), (4, 33, 3, 48), (1, 4, 19, 1040)])
 def test_combine_batch(gpu, oracle, w, G, k, rows, stride):
     import torch
     from netcode_amd import combine
@@ -41,6 +43,8 @@ def test_combine_batch(gpu, oracle, w, G, k, rows, stride):
     x = rng.integers(0, 256, (G, k, stride), dtype=np.uint8)
     cf = rng.integers(0, cmax(w), (G, k, rows), dtype=np.uint64, endpoint=True).astype(np.uint32)
     cf[0, 0, 0] = 0
+    if k > 2:
+        cf[-1, 1, :] = 0                          # a source no row uses (skipped by the wave)
     out = combine(w, torch.from_numpy(x).to(gpu), torch.from_numpy(cf.view(np.int32)).to(gpu))
     torch.cuda.synchronize()
     got = out.cpu().numpy()

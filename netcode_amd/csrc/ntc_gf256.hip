@@ -22,11 +22,11 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstdint>
-#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "gf256_field.hh"
 #include "engine.hh"
@@ -2023,60 +2023,90 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
       }
       if (lane < rp) pout[lane] = lane < m ? miss[lane] : 0;
       wave_sync();
-      // Positions m .. k-1: received sources ascending, D[s][j] = sum_q Minv[s][q] * c(q, j)
+      // Positions m .. k-1: received sources ascending, D[s][j] = sum_q Minv[s][q] * c(q, j).
+      // Two 64-source chunks per pass (lane = source base + lane and base + 64 + lane): column
+      // q's selector words are read across lanes and formed on the scalar unit once for both.
+      // (k <= 64: one chunk, the pass without the second one's registers)
       uint32_t pos_base = m;
-      for (uint32_t base = 0; base < k; base += 64) {
-        const uint32_t j = base + lane;
-        const bool got = j < k && mask_at(base) != 0;
-        const uint32_t len_j = base == 0 ? slv[0] : base == 64 ? slv[1] : (got ? slen[j] : 0u);
-        const uint64_t b = __ballot(got);
-        if (got) {
-          const uint32_t pos = pos_base + __popcll(b & lt);
-          pin[pos] = static_cast<uint16_t>(j);
-          put_row(pos, NTC_PLAN_ARG(rows_src) + (static_cast<uint64_t>(g) * k + j) * NTC_PLAN_ARG(rows_stride));
-          const uint32_t Sj = sidb + j + 1u;
-          uint32_t acc[W];
+      auto emit_pass = [&](auto two_chunks) {
+      constexpr bool kTwo = decltype(two_chunks)::value;
+      for (uint32_t base = 0; base < k; base += 128) {
+        const uint32_t j0 = base + lane, j1 = base + 64u + lane;
+        const bool got0 = j0 < k && mask_at(base) != 0;
+        const bool got1 = j1 < k && mask_at(base + 64u) != 0;
+        const uint32_t len0 = base == 0 ? slv[0] : (got0 ? slen[j0] : 0u);
+        const uint32_t len1 = base == 0 ? slv[1] : (got1 ? slen[j1] : 0u);
+        const uint64_t b0 = __ballot(got0), b1 = __ballot(got1);
+        const uint32_t pos0 = pos_base + __popcll(b0 & lt);
+        const uint32_t pos1 = pos_base + __popcll(b0) + __popcll(b1 & lt);
+        if (got0) {
+          pin[pos0] = static_cast<uint16_t>(j0);
+          put_row(pos0, NTC_PLAN_ARG(rows_src) + (static_cast<uint64_t>(g) * k + j0) * NTC_PLAN_ARG(rows_stride));
+        }
+        if (got1) {
+          pin[pos1] = static_cast<uint16_t>(j1);
+          put_row(pos1, NTC_PLAN_ARG(rows_src) + (static_cast<uint64_t>(g) * k + j1) * NTC_PLAN_ARG(rows_stride));
+        }
+        const bool two = kTwo && b1 != 0;                  // wave-uniform
+        const uint32_t Sa = sidb + j0 + 1u, Sb = sidb + j1 + 1u;
+        uint32_t acc0[W], acc1[W];
 #pragma unroll
-          for (int w = 0; w < W; ++w) acc[w] = 0;
-          const uint32_t mq = m;
-          // the coefficient table of q+1 is looked up while q's products are formed (its LDS
-          // gather is issued after q's selector loads, so their wait leaves it in flight)
-          uint32_t tn[5] = {0, 0, 0, 0, 0};
-          if (mq) {
-            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, 0);
-            tab(((R1 + Sj) * R1) % 255u + 1u, tn);
+        for (int w = 0; w < W; ++w) acc0[w] = acc1[w] = 0;
+        const uint32_t mq = m;
+        // the coefficient tables of q+1 are looked up while q's products are formed (their LDS
+        // gathers are issued after q's selector reads, so their wait leaves them in flight)
+        uint32_t tn0[5] = {0, 0, 0, 0, 0}, tn1[5] = {0, 0, 0, 0, 0};
+        if (mq) {
+          const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, 0);
+          tab(((R1 + Sa) * R1) % 255u + 1u, tn0);
+          if (two) tab(((R1 + Sb) * R1) % 255u + 1u, tn1);
+        }
+        for (uint32_t q = 0; q < mq; ++q) {
+          uint32_t tc0[5], tc1[5];
+#pragma unroll
+          for (int e = 0; e < 5; ++e) { tc0[e] = tn0[e]; tc1[e] = tn1[e]; }
+          // column q's selector words, uniform: M^-1 column q is lane RM + q's col[] (read across
+          // lanes), its v_perm selectors formed on the scalar unit.  Broadcast LDS reads of them
+          // (6 x 16 B per lane and q) saturated the CU's LDS with 16 waves in this loop.
+          uint32_t sq[3][W];
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const uint32_t cw = __builtin_amdgcn_readlane(col[w], RM + q);
+            sq[0][w] = cw & 0x07070707u;
+            sq[1][w] = (cw >> 3) & 0x07070707u;
+            sq[2][w] = (cw >> 6) & 0x03030303u;
           }
-          for (uint32_t q = 0; q < mq; ++q) {
-            uint32_t tc[5];
+          if (q + 1 < mq) {
+            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q + 1);
+            tab(((R1 + Sa) * R1) % 255u + 1u, tn0);
+            if (two) tab(((R1 + Sb) * R1) % 255u + 1u, tn1);
+          }
 #pragma unroll
-            for (int e = 0; e < 5; ++e) tc[e] = tn[e];
-            // column q's selector words, uniform: M^-1 column q is lane m + q's col[] (read
-            // across lanes, v_readlane works whatever EXEC holds), its v_perm selectors formed on
-            // the scalar unit.  Broadcast LDS reads of them (6 x 16 B per lane and q) saturated
-            // the CU's LDS with 16 waves in this loop.
-            uint32_t sq[3][W];
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-              const uint32_t cw = __builtin_amdgcn_readlane(col[w], RM + q);
-              sq[0][w] = cw & 0x07070707u;
-              sq[1][w] = (cw >> 3) & 0x07070707u;
-              sq[2][w] = (cw >> 6) & 0x03030303u;
-            }
-            if (q + 1 < mq) {
-              const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q + 1);
-              tab(((R1 + Sj) * R1) % 255u + 1u, tn);
-            }
+          for (int w = 0; w < W; ++w)
+            acc0[w] ^= xor3(__builtin_amdgcn_perm(tc0[1], tc0[0], sq[0][w]),
+                            __builtin_amdgcn_perm(tc0[3], tc0[2], sq[1][w]),
+                            __builtin_amdgcn_perm(tc0[4], tc0[4], sq[2][w]));
+          if (two) {
 #pragma unroll
             for (int w = 0; w < W; ++w)
-              acc[w] ^= xor3(__builtin_amdgcn_perm(tc[1], tc[0], sq[0][w]),
-                               __builtin_amdgcn_perm(tc[3], tc[2], sq[1][w]),
-                               __builtin_amdgcn_perm(tc[4], tc[4], sq[2][w]));
+              acc1[w] ^= xor3(__builtin_amdgcn_perm(tc1[1], tc1[0], sq[0][w]),
+                              __builtin_amdgcn_perm(tc1[3], tc1[2], sq[1][w]),
+                              __builtin_amdgcn_perm(tc1[4], tc1[4], sq[2][w]));
           }
-          emit(pos, acc);
-          size_terms(len_j, acc);
         }
-        pos_base += __popcll(b);
+        if (got0) {
+          emit(pos0, acc0);
+          size_terms(len0, acc0);
+        }
+        if (got1) {
+          emit(pos1, acc1);
+          size_terms(len1, acc1);
+        }
+        pos_base += __popcll(b0) + __popcll(b1);
       }
+      };
+      if (k > 64) emit_pass(std::true_type{});
+      else emit_pass(std::false_type{});
       // XOR-reduce the size terms over the wave; lane s < m keeps byte s
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1)

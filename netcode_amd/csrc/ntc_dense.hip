@@ -391,7 +391,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         for (int e = 0; e < 9; ++e) {
           uint32_t val = __builtin_amdgcn_readlane(v[wd(e)], first);
           if (wd(e) == 8 + q) val ^= 1u << sh;
-          x = lane == static_cast<uint32_t>(e) ? val : x;
+          asm("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(val), "i"(e));   // lane e of the record
         }
         u32x4 ti;
         ti[0] = __builtin_amdgcn_readlane(tl[0], first);

@@ -195,15 +195,60 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
   bool elig = row_ok && a.flag[gi] != 0;
   const uint32_t cp = a.c0 - kPanel;                   // LOOKAHEAD: the previous panel's columns
   if (LOOKAHEAD && g == 0) DN_CLK(a.c0 / kPanel, 0);
-  stage_tab(sm.perm_t, dn_perm, i, nthreads);
-  stage_tab(sm.pinv_t, dn_pinv, i, nthreads);
-  if (LOOKAHEAD) {
-    const uint32_t* pivp = a.piv + static_cast<size_t>(g) * np + cp;
-    for (uint32_t e = i; e < kPanel * 8; e += nthreads) {
-      const uint32_t s = e >> 3, d = e & 7;
-      const size_t prow = static_cast<size_t>(g) * np + pivp[s];
-      sm.tsel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d));
-      sm.psel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.X + prow * P + a.c0 + 4 * d));
+  // LOOKAHEAD with >= 256 threads: two rounds of loads before the staging barrier -- (1) the
+  // previous pivots, all row flags (16 per lane) and the tables; (2) the pivot rows' T and panel
+  // words, and the owner rows' words the derivation needs (the owner = the wave of the lowest
+  // eligible row, known from the flags), so the derivation starts with its operands in registers
+  uint32_t owner_e = 0, xq0 = 0, xq1 = 0;
+  u32x4 own0 = {0, 0, 0, 0}, own1 = {0, 0, 0, 0};
+  const bool early = LOOKAHEAD && nthreads >= kPanel * 8;
+  if (early) {
+    const bool st = i < kPanel * 8;
+    const uint32_t s_ = i >> 3, d_ = i & 7u;
+    const uint32_t pr = st ? a.piv[static_cast<size_t>(g) * np + cp + s_] : 0u;
+    const uint32_t r0 = lane * 16u;
+    u32x4 fl = {0, 0, 0, 0};
+    if (r0 < np) fl = *reinterpret_cast<const u32x4*>(a.flag + static_cast<size_t>(g) * np + r0);
+    stage_tab(sm.perm_t, dn_perm, i, nthreads);
+    stage_tab(sm.pinv_t, dn_pinv, i, nthreads);
+    uint32_t fidx = ~0u;
+#pragma unroll
+    for (int d = 3; d >= 0; --d)
+      if (fl[d] != 0) fidx = 4u * d + (__builtin_ctz(fl[d]) >> 3);
+    const uint64_t fb = __ballot(fidx != ~0u);
+    if (fb != 0) {
+      const uint32_t fl_lane = __ffsll(static_cast<long long>(fb)) - 1;
+      owner_e = (16u * fl_lane + __builtin_amdgcn_readlane(fidx, fl_lane)) >> 6;
+    }
+    owner_e = __builtin_amdgcn_readfirstlane(owner_e);
+    const uint32_t orow = owner_e * 64u + lane;
+    if (orow < np) {
+      const uint8_t* xo = a.X + (static_cast<size_t>(g) * np + orow) * P;
+      if (w < kPanel) xq0 = *reinterpret_cast<const uint32_t*>(xo + cp + (w & ~3u));
+      if (w + nw < kPanel) xq1 = *reinterpret_cast<const uint32_t*>(xo + cp + ((w + nw) & ~3u));
+      if (w == owner_e) {
+        own0 = reinterpret_cast<const u32x4*>(xo + a.c0)[0];
+        own1 = reinterpret_cast<const u32x4*>(xo + a.c0)[1];
+      }
+    }
+    if (st) {
+      const size_t prow = static_cast<size_t>(g) * np + pr;
+      const uint32_t wv = *reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d_);
+      const uint32_t xv = *reinterpret_cast<const uint32_t*>(a.X + prow * P + a.c0 + 4 * d_);
+      sm.tsel[s_][d_] = sel4(wv);
+      sm.psel[s_][d_] = sel4(xv);
+    }
+  } else {
+    stage_tab(sm.perm_t, dn_perm, i, nthreads);
+    stage_tab(sm.pinv_t, dn_pinv, i, nthreads);
+    if (LOOKAHEAD) {
+      const uint32_t* pivp = a.piv + static_cast<size_t>(g) * np + cp;
+      for (uint32_t e = i; e < kPanel * 8; e += nthreads) {
+        const uint32_t s = e >> 3, d = e & 7;
+        const size_t prow = static_cast<size_t>(g) * np + pivp[s];
+        sm.tsel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d));
+        sm.psel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.X + prow * P + a.c0 + 4 * d));
+      }
     }
   }
   if (i < 2) sm.cm[i] = 0;
@@ -215,8 +260,9 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
   __syncthreads();
   if (LOOKAHEAD && g == 0) DN_CLK(a.c0 / kPanel, 1);
   if (!live) return;                                   // uniform: a singular generation stops
-  uint32_t owner = 0;
-  for (uint32_t q = nw; q-- > 0;) owner = sm.ne[q] ? q : owner;
+  uint32_t owner = owner_e;
+  if (!early)
+    for (uint32_t q = nw; q-- > 0;) owner = sm.ne[q] ? q : owner;
   owner = __builtin_amdgcn_readfirstlane(owner);
 
   uint32_t v[16];
@@ -237,8 +283,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
     const uint32_t orow = owner * 64u + lane;
     const bool orow_ok = orow < np;
     const size_t go = static_cast<size_t>(g) * np + (orow_ok ? orow : 0u);
-    u32x4 own0 = {0, 0, 0, 0}, own1 = {0, 0, 0, 0};
-    if (w == owner && orow_ok) {
+    if (!early && w == owner && orow_ok) {
       const u32x4* src = reinterpret_cast<const u32x4*>(a.X + go * P + a.c0);
       own0 = src[0];
       own1 = src[1];
@@ -259,7 +304,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
     {
       uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (uint32_t s = w; s < kPanel; s += nw) {
-        const uint32_t xq = orow_ok ? *reinterpret_cast<const uint32_t*>(a.X + go * P + cp + (s & ~3u)) : 0u;
+        const uint32_t xq = early && s == w ? xq0 : early && s == w + nw ? xq1
+                          : orow_ok ? *reinterpret_cast<const uint32_t*>(a.X + go * P + cp + (s & ~3u)) : 0u;
         const uint32_t b = (xq >> (8 * (s & 3))) & 0xFFu;
         const u32x4 tf = sm.perm_t.a[b];
         const uint32_t tf4 = sm.perm_t.b[b];

@@ -78,6 +78,12 @@ __device__ __forceinline__ void stage_tab(LdsTab& t, const PermTables& src, uint
   }
 }
 
+__device__ __forceinline__ uint32_t lds_addr(const void* p)
+{
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      reinterpret_cast<const __attribute__((address_space(3))) uint8_t*>(reinterpret_cast<uintptr_t>(p))));
+}
+
 template <typename T>
 __device__ __forceinline__ T const_load(const void* p)
 {
@@ -433,42 +439,50 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       for (int e = 0; e < 9; ++e) v[wd(e)] ^= mul_sel(tf, tf4, sm.rec[s][e]);
     }
   };
-  // the owner's form: the row's table tf (of its column-s byte) was fetched at the start of the
-  // step, before the record exists, and the pivot row takes the record by a select, not a branch.
-  // (Round 4 measured two alternatives slower at n = 1024: the record as v_readlane'd uniform
-  // dwords instead of an LDS round trip, 0.888 -> 0.961 ms, and one branch-free basic block per
-  // phase, -> 1.04 ms.)
-  auto apply_own = [&](int s, bool pivot, const u32x4 tf, uint32_t tf4) {
-    const int q = s >> 2;
-    auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      const u32x4 c4 = sm.rec[s][e];
-      const uint32_t upd = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
-                                                       __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
-                           __builtin_amdgcn_perm(tf4, tf4, c4[3]);
-      v[wd(e)] = pivot ? c4[0] : upd;
-    }
-  };
-
   uint32_t t = 0;
   for (uint32_t phase = 0;; ++phase) {
     const uint32_t par = phase & 1u;
     if (w == owner) {                                    // wave-uniform: run ahead from step t
+      // One step: ballot of the rows with a non-zero in column s, the pivot row's nine window
+      // words into lanes 0-8 (v_readlane -> v_writelane), normalised there by the pivot's 1/f
+      // table (v_readlane'd from its lane) and written to LDS as the step's record with its v_perm
+      // selectors, then every row's update from the record (the pivot row takes the record by a
+      // select).  Software-pipelined: step s + 1's table gathers are issued right after the word
+      // of column s + 1 is updated and land under the rest of step s's update.  Those gathers and
+      // the record reads are inline asm, so the compiler can neither sink the gathers below the
+      // next ballot nor make a record read wait on them (LDS returns in order: every record read
+      // is issued before the gathers).  Measured slower (round 4): the record as v_readlane'd
+      // uniform words with scalar selectors instead of the LDS round trip, one branch-free block
+      // per phase, and the same pipelining with compiler-placed loads.
       uint32_t stop = kPanel;
+      const uint32_t pa0 = lds_addr(&sm.perm_t.a[0]), pb0 = lds_addr(&sm.perm_t.b[0]);
+      const uint32_t ia0 = lds_addr(&sm.pinv_t.a[0]), ib0 = lds_addr(&sm.pinv_t.b[0]);
+      const uint32_t rec0 = lds_addr(&sm.rec[0][0]);
+      u32x4 tfn, tln;
+      uint32_t tf4n, tl4n;
+      auto gather = [&](uint32_t fv) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(tfn) : "v"(pa0 + 16u * fv));
+        asm volatile("ds_read_b32 %0, %1" : "=v"(tf4n) : "v"(pb0 + 4u * fv));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(tln) : "v"(ia0 + 16u * fv));
+        asm volatile("ds_read_b32 %0, %1" : "=v"(tl4n) : "v"(ib0 + 4u * fv));
+      };
+      uint32_t fn = 0;
+#pragma unroll
+      for (int s = 0; s < static_cast<int>(kPanel); ++s)
+        if (s == static_cast<int>(t)) fn = (v[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+      gather(fn);
+      uint64_t elig_m = __ballot(elig);                 // the eligible rows as a wave mask
+      uint32_t pv = 0;                                   // lane s: the pivot row of step s
 #pragma unroll
       for (int s = 0; s < static_cast<int>(kPanel); ++s) {
         if (s < static_cast<int>(t)) continue;
         const int q = s >> 2, sh = 8 * (s & 3);
         auto wd = [q](int e) { return e < 8 - q ? q + e : 8 + (e - (8 - q)); };
-        const uint32_t f = (v[q] >> sh) & 0xFFu;
-        const u32x4 tf = sm.perm_t.a[f];   // f = 0: all-zero table
-        const uint32_t tf4 = sm.perm_t.b[f];
-        // every row's 1/f table too: the pivot's is then read from its lane (readlane), not
-        // looked up after the pivot is known
-        const u32x4 tl = sm.pinv_t.a[f];
-        const uint32_t tl4 = sm.pinv_t.b[f];
-        const uint64_t b = __ballot(elig && f != 0);
+        const uint32_t f = fn;
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tfn), "+v"(tf4n), "+v"(tln), "+v"(tl4n));
+        const u32x4 tf = tfn, tl = tln;
+        const uint32_t tf4 = tf4n, tl4 = tl4n;
+        const uint64_t b = __ballot(f != 0) & elig_m;
         if (b == 0) { stop = s; break; }
         const uint32_t first = __ffsll(static_cast<long long>(b)) - 1;
         uint32_t x = 0;
@@ -476,7 +490,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         for (int e = 0; e < 9; ++e) {
           uint32_t val = __builtin_amdgcn_readlane(v[wd(e)], first);
           if (wd(e) == 8 + q) val ^= 1u << sh;
-          asm("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(val), "i"(e));   // lane e of the record
+          asm("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(val), "i"(e));
         }
         u32x4 ti;
         ti[0] = __builtin_amdgcn_readlane(tl[0], first);
@@ -485,13 +499,44 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         ti[3] = __builtin_amdgcn_readlane(tl[3], first);
         const uint32_t ti4 = __builtin_amdgcn_readlane(tl4, first);
         if (lane < 9) sm.rec[s][lane] = sel4(mul4(ti[0], ti[1], ti[2], ti[3], ti4, x));
-        __builtin_amdgcn_wave_barrier();                 // this wave's record writes before its reads
-        const uint32_t prow = w * 64u + first;
-        if (lane == 0) a.piv[static_cast<size_t>(g) * np + a.c0 + s] = prow;
+        __builtin_amdgcn_wave_barrier();
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(pv) : "s"(__builtin_amdgcn_readfirstlane(w * 64u + first)), "i"(s));
         const bool me = lane == first;
-        apply_own(s, me, tf, tf4);
+        const int en = (s + 1 < static_cast<int>(kPanel)) ? (((s + 1) >> 2) - q) : 0;
+        // the record's nine entries read by inline asm too, the next column's first, so that
+        // every read is older than the next step's gathers (LDS returns in order: waiting for the
+        // record never waits for the gathers)
+        u32x4 c[9];
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(c[en]) : "v"(rec0), "i"((s * 9 + en) * 16));
+#pragma unroll
+        for (int e = 0; e < 9; ++e)
+          if (e != en) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(c[e]) : "v"(rec0), "i"((s * 9 + e) * 16));
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(c[en]));
+        auto upd = [&](int e) {
+          const u32x4 c4 = c[e];
+          const uint32_t u = __builtin_amdgcn_bitop3_b32(v[wd(e)], __builtin_amdgcn_perm(tf[1], tf[0], c4[1]),
+                                                         __builtin_amdgcn_perm(tf[3], tf[2], c4[2]), 0x96) ^
+                             __builtin_amdgcn_perm(tf4, tf4, c4[3]);
+          v[wd(e)] = me ? c4[0] : u;
+        };
+        upd(en);
+        if (s + 1 < static_cast<int>(kPanel)) {
+          fn = (v[(s + 1) >> 2] >> (8 * ((s + 1) & 3))) & 0xFFu;
+          gather(fn);
+          asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]),
+                       "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]));
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]),
+                       "+v"(c[5]), "+v"(c[6]), "+v"(c[7]), "+v"(c[8]));
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e)
+          if (e != en) upd(e);
+        elig_m &= ~(1ull << first);
         if (me) { chosen = true; elig = false; }
       }
+      // this phase's pivots, one store
+      if (lane >= t && lane < stop) a.piv[static_cast<size_t>(g) * np + a.c0 + lane] = pv;
       if (lane == 0) sm.stopv[par] = stop;
     }
     __syncthreads();

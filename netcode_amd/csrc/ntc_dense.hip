@@ -188,8 +188,8 @@ struct PanelSmem {
 // from the pre-update matrix -- W_i = X_i[prev panel] * T, then X_i[panel] ^= sum_t W_i[t] *
 // X[piv_t][panel], the update's own arithmetic, split over all waves -- and the other waves derive
 // their own rows only if the owner does not finish the panel alone (an election).
-// LOOKAHEAD: part = dynamic LDS of 2nw x 8 x 64 dwords at nw = 8 / 16 (per wave: phase-1 partial
-// words, then phase-2 partials), (nw + 1) x 8 x 64 otherwise (partials, then their XOR)
+// LOOKAHEAD: part = dynamic LDS of 2 x 8 x 64 dwords at nw = 8 / 16 (the two ds_xor regions),
+// (nw + 1) x 8 x 64 otherwise (per wave partial words, then their XOR)
 template <bool LOOKAHEAD>
 __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uint32_t g, uint32_t i,
                                           uint32_t nthreads, uint32_t* part = nullptr)
@@ -237,6 +237,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         own1 = reinterpret_cast<const u32x4*>(xo + a.c0)[1];
       }
     }
+    if (nw == 16u || nw == 8u)                         // the ds_xor regions of the derivation
+      for (uint32_t e = i; e < 2u * 8u * 64u; e += nthreads) part[e] = 0;
     if (st) {
       const size_t prow = static_cast<size_t>(g) * np + pr;
       const uint32_t wv = *reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d_);
@@ -318,20 +320,22 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
         for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.tsel[s][d]);
       }
+      if (nw == 16u || nw == 8u) {
 #pragma unroll
-      for (int d = 0; d < 8; ++d) pa[(w * 8u + d) * 64u + lane] = acc[d];
+        for (int d = 0; d < 8; ++d)
+          __hip_atomic_fetch_xor(&part[d * 64u + lane], acc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+#pragma unroll
+        for (int d = 0; d < 8; ++d) pa[(w * 8u + d) * 64u + lane] = acc[d];
+      }
     }
     __syncthreads();
     if (nw == 16u || nw == 8u) {
-      // phase 2 with one W_i word per wave: wave w takes the terms t0 .. t0 + 32/nw - 1, all in
-      // word t0 / 4, which it reduces from the phase-1 partials itself; its 8 partial words go to
-      // region C ([nw][2][64] 16-byte pieces) and only the owner wave reduces those: two barriers
-      // instead of four
+      // 8 or 16 waves: the partial words are XOR-accumulated in LDS (ds_xor) -- region 1 = W_i,
+      // region 2 = the owner rows' panel words -- and phase 2 gives each wave one W_i word: wave w
+      // takes the terms t0 .. t0 + 32/nw - 1, which all sit in word t0 / 4
       const uint32_t tpw = kPanel / nw, t0 = w * tpw, dw = t0 >> 2;
-      uint32_t y = 0;
-#pragma unroll
-      for (uint32_t u = 0; u < 16; ++u)
-        if (u < nw) y ^= pa[(u * 8u + dw) * 64u + lane];
+      const uint32_t y = part[dw * 64u + lane];
       uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (uint32_t j = 0; j < tpw; ++j) {
         const uint32_t t = t0 + j;
@@ -341,22 +345,14 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
         for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.psel[t][d]);
       }
-      u32x4* pc = reinterpret_cast<u32x4*>(part + nw * 8u * 64u);
-      pc[(w * 2u) * 64u + lane] = u32x4{acc[0], acc[1], acc[2], acc[3]};
-      pc[(w * 2u + 1u) * 64u + lane] = u32x4{acc[4], acc[5], acc[6], acc[7]};
+#pragma unroll
+      for (int d = 0; d < 8; ++d)
+        __hip_atomic_fetch_xor(&part[512u + d * 64u + lane], acc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __syncthreads();
       if (w == owner) {
-        u32x4 r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+        const uint32_t x8[8] = {own0[0], own0[1], own0[2], own0[3], own1[0], own1[1], own1[2], own1[3]};
 #pragma unroll
-        for (uint32_t u = 0; u < 16; ++u)
-          if (u < nw) {
-            r0 ^= pc[(u * 2u) * 64u + lane];
-            r1 ^= pc[(u * 2u + 1u) * 64u + lane];
-          }
-        const uint32_t x8[8] = {own0[0] ^ r0[0], own0[1] ^ r0[1], own0[2] ^ r0[2], own0[3] ^ r0[3],
-                                own1[0] ^ r1[0], own1[1] ^ r1[1], own1[2] ^ r1[2], own1[3] ^ r1[3]};
-#pragma unroll
-        for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] : 0u;
+        for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ part[512u + d * 64u + lane] : 0u;
         have = true;
       }
     } else {
@@ -859,11 +855,11 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
       const uint64_t spread = G < 240 ? 240 - G : 16;
       fa.tpb = static_cast<uint32_t>(std::min<uint64_t>(nw, std::max<uint64_t>(1, (waves + spread - 1) / spread)));
       const uint64_t nb = (waves + fa.tpb - 1) / fa.tpb;
-      // phase-1 partials + phase-2 partials (nw = 8, 16) or the reduced words (otherwise)
-      const size_t part_bytes = static_cast<size_t>(nw == 16 || nw == 8 ? 2 * nw : nw + 1) * 8 * 64 * 4;
+      // the two ds_xor regions (nw = 8, 16) or the partials + reduced words (otherwise)
+      const size_t part_bytes = static_cast<size_t>(nw == 16 || nw == 8 ? 2 : nw + 1) * 8 * 64 * 4;
       static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(dn_fused),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   static_cast<int>(32 * 8 * 64 * 4)) == hipSuccess;
+                                                   static_cast<int>(17 * 8 * 64 * 4)) == hipSuccess;
       (void)attr;
       hipLaunchKernelGGL(dn_fused, dim3(static_cast<uint32_t>(G + nb)), dim3(threads), part_bytes, st, fa);
       if ((rc = hip_check(hipGetLastError(), "dn_fused launch"))) return rc;

@@ -147,3 +147,37 @@ def test_dense_config5_round_trip(gpu):
     torch.cuda.synchronize(gpu)
     assert int(ok.item()) == 1
     assert torch.equal(out, src)
+
+
+def test_dense_invert_xor_derivation_sizes(gpu, oracle):
+    """The 8-wave lookahead derivation (ds_xor accumulation) with a ragged last wave (n = 480:
+    rows 480-511 of the block are padding) and a singular generation among three."""
+    import torch
+    from netcode_amd import DenseCode
+    G, n = 3, 480
+    mats = _mats(G, n, seed=480, singular=(1,))
+    inv, ok = DenseCode(gpu).invert(_dev(mats, gpu))
+    torch.cuda.synchronize(gpu)
+    inv, ok = inv.cpu().numpy(), ok.cpu().numpy()
+    for g in range(G):
+        o_ok, _, o_inv = oracle.dense_decode(mats[g], np.zeros((n, 16), np.uint8))
+        assert bool(ok[g]) == o_ok, g
+        assert (inv[g] == o_inv).all(), g
+
+
+def test_dense_round_trip_16_waves_two_generations(gpu):
+    """The 16-wave derivation (n = 1000, padded to 1024) for two generations, one singular: the
+    invertible one round-trips, the singular one is reported as such."""
+    import torch
+    from netcode_amd import DenseCode
+    dc = DenseCode(gpu)
+    G, k, S = 2, 1000, 1024
+    g = torch.Generator(device=gpu).manual_seed(6)
+    src = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=gpu, generator=g)
+    mats = _mats(G, k, seed=1000, singular=(1,))
+    mat = _dev(mats, gpu)
+    rep = dc.encode(mat, src)
+    out, ok = dc.decode(mat, rep)
+    torch.cuda.synchronize(gpu)
+    assert ok.cpu().numpy().tolist() == [1, 0]
+    assert torch.equal(out[0], src[0])

@@ -188,8 +188,7 @@ struct PanelSmem {
 // from the pre-update matrix -- W_i = X_i[prev panel] * T, then X_i[panel] ^= sum_t W_i[t] *
 // X[piv_t][panel], the update's own arithmetic, split over all waves -- and the other waves derive
 // their own rows only if the owner does not finish the panel alone (an election).
-// LOOKAHEAD: part = dynamic LDS of 2 x 8 x 64 dwords at nw = 8 / 16 (the two ds_xor regions),
-// (nw + 1) x 8 x 64 otherwise (per wave partial words, then their XOR)
+// LOOKAHEAD: part = dynamic LDS of 2 x 8 x 64 dwords (the derivation's two ds_xor regions)
 template <bool LOOKAHEAD>
 __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uint32_t g, uint32_t i,
                                           uint32_t nthreads, uint32_t* part = nullptr)
@@ -237,8 +236,6 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         own1 = reinterpret_cast<const u32x4*>(xo + a.c0)[1];
       }
     }
-    if (nw == 16u || nw == 8u)                         // the ds_xor regions of the derivation
-      for (uint32_t e = i; e < 2u * 8u * 64u; e += nthreads) part[e] = 0;
     if (st) {
       const size_t prow = static_cast<size_t>(g) * np + pr;
       const uint32_t wv = *reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d_);
@@ -259,6 +256,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       }
     }
   }
+  if (LOOKAHEAD)                                       // the derivation's two ds_xor regions
+    for (uint32_t e = i; e < 2u * 8u * 64u; e += nthreads) part[e] = 0;
   if (i < 2) sm.cm[i] = 0;
   {
     const uint64_t e0 = __ballot(elig);
@@ -287,7 +286,8 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
   } else {
     // the owner's 64 rows, all waves: wave w takes the terms s = w, w + nw, ... of W_i (phase 1)
     // and then of the panel columns (phase 2), all 8 words each -- every table is gathered once
-    // per lane -- and the words are XOR-reduced over the waves' partials in LDS
+    // per lane -- and XOR-accumulates its partial words into LDS (ds_xor): region 1 = W_i,
+    // region 2 = the owner rows' panel words, zeroed before the staging barrier
     const uint32_t orow = owner * 64u + lane;
     const bool orow_ok = orow < np;
     const size_t go = static_cast<size_t>(g) * np + (orow_ok ? orow : 0u);
@@ -296,18 +296,10 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       own0 = src[0];
       own1 = src[1];
     }
-    // part: region A = [nw][8][64] partial words, region B = [8][64] reduced words
-    uint32_t* pa = part;
-    uint32_t* pb = part + nw * 8u * 64u;
-    // XOR of the nw partials of word d, written to B (waves share the 8 words)
-    auto reduce_words = [&]() {
-      for (uint32_t d = w; d < 8; d += nw) {
-        uint32_t y = 0;
+    auto xor_words = [&](uint32_t* region, const uint32_t (&acc)[8]) {
 #pragma unroll
-        for (uint32_t u = 0; u < 16; ++u)
-          if (u < nw) y ^= pa[(u * 8u + d) * 64u + lane];
-        pb[d * 64u + lane] = y;
-      }
+      for (int d = 0; d < 8; ++d)
+        __hip_atomic_fetch_xor(&region[d * 64u + lane], acc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     {
       uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -320,65 +312,26 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
 #pragma unroll
         for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.tsel[s][d]);
       }
-      if (nw == 16u || nw == 8u) {
-#pragma unroll
-        for (int d = 0; d < 8; ++d)
-          __hip_atomic_fetch_xor(&part[d * 64u + lane], acc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-#pragma unroll
-        for (int d = 0; d < 8; ++d) pa[(w * 8u + d) * 64u + lane] = acc[d];
-      }
+      xor_words(part, acc);
     }
-    __syncthreads();
-    if (nw == 16u || nw == 8u) {
-      // 8 or 16 waves: the partial words are XOR-accumulated in LDS (ds_xor) -- region 1 = W_i,
-      // region 2 = the owner rows' panel words -- and phase 2 gives each wave one W_i word: wave w
-      // takes the terms t0 .. t0 + 32/nw - 1, which all sit in word t0 / 4
-      const uint32_t tpw = kPanel / nw, t0 = w * tpw, dw = t0 >> 2;
-      const uint32_t y = part[dw * 64u + lane];
-      uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (uint32_t j = 0; j < tpw; ++j) {
-        const uint32_t t = t0 + j;
-        const uint32_t b = (y >> (8 * (t & 3))) & 0xFFu;
-        const u32x4 tf = sm.perm_t.a[b];
-        const uint32_t tf4 = sm.perm_t.b[b];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.psel[t][d]);
-      }
-#pragma unroll
-      for (int d = 0; d < 8; ++d)
-        __hip_atomic_fetch_xor(&part[512u + d * 64u + lane], acc[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __syncthreads();
-      if (w == owner) {
-        const uint32_t x8[8] = {own0[0], own0[1], own0[2], own0[3], own1[0], own1[1], own1[2], own1[3]};
-#pragma unroll
-        for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ part[512u + d * 64u + lane] : 0u;
-        have = true;
-      }
-    } else {
-    reduce_words();                                      // B = W_i
     __syncthreads();
     {
       uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (uint32_t t = w; t < kPanel; t += nw) {
-        const uint32_t b = (pb[(t >> 2) * 64u + lane] >> (8 * (t & 3))) & 0xFFu;
+        const uint32_t b = (part[(t >> 2) * 64u + lane] >> (8 * (t & 3))) & 0xFFu;
         const u32x4 tf = sm.perm_t.a[b];
         const uint32_t tf4 = sm.perm_t.b[b];
 #pragma unroll
         for (int d = 0; d < 8; ++d) acc[d] ^= mul_sel(tf, tf4, sm.psel[t][d]);
       }
-#pragma unroll
-      for (int d = 0; d < 8; ++d) pa[(w * 8u + d) * 64u + lane] = acc[d];
+      xor_words(part + 512u, acc);
     }
-    __syncthreads();
-    reduce_words();                                      // B = sum_t W_i[t] X[piv_t][panel]
     __syncthreads();
     if (w == owner) {
       const uint32_t x8[8] = {own0[0], own0[1], own0[2], own0[3], own1[0], own1[1], own1[2], own1[3]};
 #pragma unroll
-      for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ pb[d * 64u + lane] : 0u;
+      for (int d = 0; d < 8; ++d) v[d] = orow_ok ? x8[d] ^ part[512u + d * 64u + lane] : 0u;
       have = true;
-    }
     }
     if (g == 0) DN_CLK(a.c0 / kPanel, 2);
   }
@@ -855,8 +808,7 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
       const uint64_t spread = G < 240 ? 240 - G : 16;
       fa.tpb = static_cast<uint32_t>(std::min<uint64_t>(nw, std::max<uint64_t>(1, (waves + spread - 1) / spread)));
       const uint64_t nb = (waves + fa.tpb - 1) / fa.tpb;
-      // the two ds_xor regions (nw = 8, 16) or the partials + reduced words (otherwise)
-      const size_t part_bytes = static_cast<size_t>(nw == 16 || nw == 8 ? 2 : nw + 1) * 8 * 64 * 4;
+      const size_t part_bytes = 2 * 8 * 64 * 4;        // the derivation's two ds_xor regions
       static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(dn_fused),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    static_cast<int>(17 * 8 * 64 * 4)) == hipSuccess;

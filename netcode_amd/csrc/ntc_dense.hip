@@ -210,7 +210,10 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
   if (early) {
     const bool st = i < kPanel * 8;
     const uint32_t s_ = i >> 3, d_ = i & 7u;
-    const uint32_t pr = st ? a.piv[static_cast<size_t>(g) * np + cp + s_] : 0u;
+    // a generation that went singular stopped writing pivots (and one that was singular from the
+    // start never wrote any): its entries are stale or uninitialised, so clamp them into the
+    // generation's rows -- the words loaded for a dead generation are never used (!live below)
+    const uint32_t pr = st ? min(a.piv[static_cast<size_t>(g) * np + cp + s_], np - 1u) : 0u;
     const uint32_t r0 = lane * 16u;
     u32x4 fl = {0, 0, 0, 0};
     if (r0 < np) fl = *reinterpret_cast<const u32x4*>(a.flag + static_cast<size_t>(g) * np + r0);
@@ -250,7 +253,7 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
       const uint32_t* pivp = a.piv + static_cast<size_t>(g) * np + cp;
       for (uint32_t e = i; e < kPanel * 8; e += nthreads) {
         const uint32_t s = e >> 3, d = e & 7;
-        const size_t prow = static_cast<size_t>(g) * np + pivp[s];
+        const size_t prow = static_cast<size_t>(g) * np + min(pivp[s], np - 1u);   // as above
         sm.tsel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.W + prow * kPanel + 4 * d));
         sm.psel[s][d] = sel4(*reinterpret_cast<const uint32_t*>(a.X + prow * P + a.c0 + 4 * d));
       }

@@ -382,6 +382,49 @@ __device__ __forceinline__ void swap_blocks(uint32_t& a, uint32_t& b, uint32_t s
   b = nb;
 }
 
+// The delta-swap constants in VGPRs.  On gfx950 a VALU op issues at half rate when it reads an
+// SGPR (any slot) or has a constant in src0 (tools/gen_mb_issue.py, profiles/r05/mb_issue*.log:
+// v_bitop3 / v_xor with an SGPR, v_lshlrev_b32 with an inline-constant shift amount, v_alignbit,
+// v_lshl_or, v_bfi, v_lshlrev_b64: 4.2-4.9 cycles per SIMD; VGPR-only v_bitop3 / v_xor / v_add /
+// v_lshrrev with a VGPR amount: 2.3).  The compiler keeps constants in SGPRs and shift amounts as
+// inline constants, which would halve the transpose's rate; these come out of an asm statement,
+// so they stay in VGPRs.
+struct TMasks {
+  uint32_t m4, m2, m1;                     // 0x0F0F0F0F, 0x33333333, 0x55555555
+  uint32_t s4, s2, s1;                     // shift amounts 4, 2, 1
+};
+
+__device__ __forceinline__ TMasks tmasks()
+{
+  TMasks t;
+  asm volatile("v_mov_b32 %0, 0x0f0f0f0f\n\tv_mov_b32 %1, 0x33333333\n\tv_mov_b32 %2, 0x55555555\n\t"
+               "v_mov_b32 %3, 4\n\tv_mov_b32 %4, 2\n\tv_mov_b32 %5, 1"
+               : "=v"(t.m4), "=v"(t.m2), "=v"(t.m1), "=v"(t.s4), "=v"(t.s2), "=v"(t.s1));
+  return t;
+}
+
+// swap_blocks with VGPR operands only: m = ~(m << sh) for the three masks, so both selects use m
+__device__ __forceinline__ void swap_m(uint32_t& a, uint32_t& b, uint32_t sh, uint32_t m)
+{
+  const uint32_t na = __builtin_amdgcn_bitop3_b32(m, a, b << sh, 0xCA);     // m ? a : b << sh
+  const uint32_t nb = __builtin_amdgcn_bitop3_b32(m, a >> sh, b, 0xCA);     // m ? a >> sh : b
+  a = na;
+  b = nb;
+}
+
+__device__ __forceinline__ void transpose8(uint32_t* d, const TMasks& t)
+{
+#pragma unroll
+  for (int i = 0; i < 4; ++i) swap_m(d[i], d[i + 4], t.s4, t.m4);
+#pragma unroll
+  for (int i = 0; i < 8; i += 4) {
+    swap_m(d[i], d[i + 2], t.s2, t.m2);
+    swap_m(d[i + 1], d[i + 3], t.s2, t.m2);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) swap_m(d[i], d[i + 1], t.s1, t.m1);
+}
+
 __device__ __forceinline__ void transpose8(uint32_t* d)
 {
 #pragma unroll

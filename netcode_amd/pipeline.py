@@ -14,6 +14,7 @@ bases -- with no explicit bases, chunk generations g0..g1 get the whole-batch de
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .engine import BatchDecoder, BatchEncoder, Engine, EncodeResult, STATUS_BYTES
@@ -274,6 +275,19 @@ class HostPipeline:
                 raise ValueError(f"{name} must be {dt} {shape}, got {t.dtype} {tuple(t.shape)}")
         _pinned(h_rx_pkts, "h_rx_pkts")
         sps = h_rx_pkts.shape[1]
+        # read_packets maps a packet to generation (id - chunk's first base) // k (// r for repairs),
+        # so within every chunk the bases must be contiguous: sid[g] = sid[g0] + (g - g0)*k (mod 2^32)
+        sh = np.asarray(sid_host, dtype=np.uint64) & 0xFFFFFFFF
+        rh = np.asarray(rid_host, dtype=np.uint64) & 0xFFFFFFFF
+        if sh.shape != (G,) or rh.shape != (G,):
+            raise ValueError(f"sid_host / rid_host must hold {G} id bases")
+        for _, g0, g1 in self._chunks(G):
+            off = np.arange(g1 - g0, dtype=np.uint64)
+            if (((sh[g0:g1] - sh[g0] - off * k) & 0xFFFFFFFF) != 0).any() or \
+               (((rh[g0:g1] - rh[g0] - off * r) & 0xFFFFFFFF) != 0).any():
+                raise ValueError("encode_decode_wire needs contiguous id bases within each chunk "
+                                 f"(generations {g0}..{g1 - 1}): sid[g] = sid[g0] + (g-g0)*k, "
+                                 "rid[g] = rid[g0] + (g-g0)*r (mod 2^32)")
         _, lost_base, _, n_lost = self.row_bases(h_mask)
         wire = Wire(self.device)
         dev = self.device

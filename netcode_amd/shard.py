@@ -4,8 +4,9 @@ Generations are independent: rank ``rank`` of ``world`` owns 
 generation range [rank*G, (rank+1)*G) of one logical batch, with the same source / repair id
 bases that a single-GPU run over the whole batch would use, so every coefficient -- and hence
 every repair byte and decode outcome -- is identical to the 1-GPU result.  The only
-inter-rank traffic is a barrier and a max-reduce of the step time (torch.distributed: RCCL on
-the GPUs, gloo in the CPU tests).
+inter-rank traffic is a barrier and a max-reduce of the step time, over gloo on host tensors
+(bench.py's default on the GPUs too, so no RCCL communicator is created; NTC_BENCH_BACKEND=nccl
+selects RCCL for that reduction).
 """
 from __future__ import annotations
 

@@ -181,3 +181,31 @@ def test_dense_round_trip_16_waves_two_generations(gpu):
     torch.cuda.synchronize(gpu)
     assert ok.cpu().numpy().tolist() == [1, 0]
     assert torch.equal(out[0], src[0])
+
+
+def test_dense_invert_stale_pivots_after_large_invert(gpu, oracle):
+    """the lookahead panel reads the previous panel's pivots before it knows
+    whether the generation is still live.  A large inversion first leaves pivot indices up to
+    n - 1 = 767 in the engine's workspace; the many-generation inversion that follows has
+    generations singular from the first column (never write a pivot) and singular later (stop
+    writing them), whose stale entries must not be used as row indices."""
+    import torch
+    from netcode_amd import DenseCode
+    dc = DenseCode(gpu)
+    big = _mats(1, 768, seed=768)
+    inv, ok = dc.invert(_dev(big, gpu))
+    torch.cuda.synchronize(gpu)
+    assert int(ok.cpu().numpy()[0]) == 1
+    G, n = 48, 96
+    mats = _mats(G, n, seed=96, singular=(3, 20, 47))
+    mats[5, :, 0] = 0                      # singular at the very first column
+    mats[30, :, :40] = 0                   # singular in the second panel
+    mats[30, np.arange(32), np.arange(32)] = 1
+    inv, ok = dc.invert(_dev(mats, gpu))
+    torch.cuda.synchronize(gpu)
+    inv, ok = inv.cpu().numpy(), ok.cpu().numpy()
+    for g in range(G):
+        o_ok, _, o_inv = oracle.dense_decode(mats[g], np.zeros((n, 16), np.uint8))
+        assert bool(ok[g]) == o_ok, g
+        assert (inv[g] == o_inv).all(), g
+    assert not ok[5] and not ok[30] and not ok[3]

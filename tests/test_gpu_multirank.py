@@ -103,3 +103,69 @@ def test_bench_under_torchrun_two_ranks(tmp_path):
     assert d["verified"]["bit_exact_round_trip"]
     assert d["rank_sync"] == "gloo"                    # no RCCL for the barrier / max
     assert d["config"]["generations_per_gpu"] == 256
+
+
+def _worker_cfg4(rank, world, port, out_dir, vrank0, vworld, Gshard, k, r, S, pick):
+    """Rank `rank` plays rank vrank0 + rank of config 4's vworld-GPU run: the HIP engine encodes
+    and decodes the generations `pick` of its shard with that shard's (uint32-wrapping) ids."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    from helpers import loss_exact_m, make_sources
+    from netcode_amd import BatchDecoder, BatchEncoder, status_to_numpy
+    from netcode_amd.shard import generation_shard, max_over_ranks
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    vr = vrank0 + rank
+    sid, rid = generation_shard(vr, vworld, Gshard, k, r)
+    sid, rid = sid[pick], rid[pick]
+    n = len(pick)
+    src, lens = make_sources(n, k, S, S, seed=100 + vr, ragged=True)
+    mask = loss_exact_m(n, k, r, seed=200 + vr)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_sid, d_rid = t(sid.view(np.int32)), t(rid.view(np.int32))
+    res = BatchEncoder(k, r, dev)(t(src), t(lens.view(np.int16)), d_sid, d_rid)
+    rx = t(src * mask[:, :, None])
+    rxl = t((lens * mask).view(np.int16))
+    st = BatchDecoder(k, r, dev)(rx, rxl, t(mask), res.repairs, res.encoded_size,
+                                 torch.ones((n, r), dtype=torch.uint8, device=dev), d_sid, d_rid)
+    torch.cuda.synchronize(dev)
+    tmax = max_over_ranks(float(vr), dist, dev)
+    np.savez(os.path.join(out_dir, f"cfg4_{vr}.npz"), rep=res.repairs.cpu().numpy(),
+             rsz=res.encoded_size.cpu().numpy().view(np.uint16), out=rx.cpu().numpy(),
+             olen=rxl.cpu().numpy().view(np.uint16), st=status_to_numpy(st).view(np.uint8),
+             tmax=np.array([tmax]))
+    dist.destroy_process_group()
+
+
+def test_config4_ranks_6_7_on_the_engine(tmp_path, oracle):
+    """Config 4 (k=128 r=32, 65536 generations over 8 GPUs): two processes play ranks 6 and 7,
+    whose rid * sid products exceed 2^32 (galois_field.hh:143-158 wraps them), and run their
+    shards' generations through the HIP engine; repairs, sizes, outcomes and recovered payloads
+    equal the oracle's over the single-batch ids of the same generations."""
+    import torch.multiprocessing as mp
+    from helpers import loss_exact_m, make_sources
+    from netcode_amd.shard import generation_shard
+    vworld, Gs, k, r, S = 8, 8192, 128, 32, 1504
+    pick = np.array([0, 1, 2, Gs // 2, Gs - 3, Gs - 2, Gs - 1])
+    mp.start_processes(_worker_cfg4, args=(2, _free_port(), str(tmp_path), 6, vworld, Gs, k, r, S, pick),
+                       nprocs=2, join=True, start_method="spawn")
+    sid_all, rid_all = generation_shard(0, 1, Gs * vworld, k, r)
+    for vr in (6, 7):
+        z = np.load(os.path.join(tmp_path, f"cfg4_{vr}.npz"))
+        g = vr * Gs + pick
+        R1, S1 = rid_all[g].astype(np.uint64) + 1, sid_all[g].astype(np.uint64) + 1
+        assert ((R1 + S1) * R1 > 2**32).all()       # the wrapping products
+        n = len(pick)
+        src, lens = make_sources(n, k, S, S, seed=100 + vr, ragged=True)
+        rep, rsz = oracle.encode_batch(src, lens, k, r, sid_all[g], rid_all[g])
+        mask = loss_exact_m(n, k, r, seed=200 + vr)
+        out, olen, st = oracle.decode_batch(src * mask[:, :, None], lens * mask, mask, rep, rsz,
+                                            np.ones((n, r), np.uint8), sid_all[g], rid_all[g])
+        assert (z["rep"] == rep).all() and (z["rsz"] == rsz).all()
+        assert (z["st"].reshape(-1) == st.view(np.uint8).reshape(-1)).all()
+        assert (z["out"] == out).all() and (z["olen"] == olen).all()
+        assert float(z["tmax"][0]) == 7.0

@@ -237,3 +237,30 @@ def test_wire_pipeline_matches_oracle(gpu, G, chunk, depth, S):
     sel = dec[lost_gen]
     assert (h_rec[:n_lost].numpy()[sel] == oout[mask == 0][sel]).all()
     assert (h_dec_len.numpy().view(np.uint16)[mask == 0][sel] == olen[mask == 0][sel]).all()
+
+
+def test_wire_pipeline_rejects_non_contiguous_bases(gpu):
+    """read_packets maps ids to slots from each chunk's first bases, so encode_decode_wire refuses
+    id bases that are not contiguous within a chunk instead of misplacing packets."""
+    import torch
+    from netcode_amd import Wire
+    from netcode_amd.pipeline import HostPipeline
+    G, k, r, stride, chunk = 4, 8, 2, 64, 2
+    src = torch.zeros((G, k, stride), dtype=torch.uint8).pin_memory()
+    lens = torch.full((G, k), stride, dtype=torch.int16).pin_memory()
+    mask = torch.ones((G, k), dtype=torch.uint8).pin_memory()
+    rps, sps = Wire.repair_packet_bytes(k, stride), Wire.source_packet_bytes(stride)
+    args = (src, lens, torch.zeros((G * r, rps), dtype=torch.uint8).pin_memory(),
+            torch.zeros((G * r,), dtype=torch.int32).pin_memory(),
+            torch.zeros((G * k, sps), dtype=torch.uint8).pin_memory(),
+            torch.zeros((G * k,), dtype=torch.int32).pin_memory(),
+            torch.arange(0, G * k + 1, k), mask, torch.zeros((1, stride), dtype=torch.uint8).pin_memory(),
+            torch.zeros((G, k), dtype=torch.int16).pin_memory(),
+            torch.zeros((G, 12), dtype=torch.uint8).pin_memory())
+    sid = np.arange(G, dtype=np.uint32) * k
+    rid = np.arange(G, dtype=np.uint32) * r
+    sid[1] += 1                                     # generation 1 not at sid[0] + k
+    d = lambda a: torch.from_numpy(a.view(np.int32).copy()).to(gpu)
+    p = HostPipeline(k, r, stride, chunk, gpu, 2)
+    with pytest.raises(ValueError, match="contiguous"):
+        p.encode_decode_wire(*args, sid, rid, d(sid), d(rid))

@@ -1,6 +1,8 @@
 """N>1 path on CPU (gloo, world_size 2): generation sharding reproduces the single-process batch
 bit for bit (ids, repairs, decode outcomes), and the bench's barrier + max-time reduction works.
-The GPU ranks run the same code with backend "nccl" (RCCL) and the HIP engine."""
+The GPU ranks (bench.py --gpus N under torchrun) run the same shard code with the HIP engine and
+the same gloo barrier / max-reduce on host tensors -- no collective touches the data path.  The
+HIP engine itself is run per rank in tests/test_gpu_multirank.py."""
 import os
 import socket
 
@@ -93,10 +95,12 @@ def _worker_cfg4(rank, world, port, out_dir, vrank0, vworld, G, k, r, S, pick):
 
 
 def test_config4_last_ranks_wrapping_ids(tmp_path, oracle):
-    """Config 4 (k=128 r=32, 65536 generations over 8 GPUs): ranks 6 and 7 own the generations
-    whose rid * sid products exceed 2^32 (galois_field.hh:143-158 wraps them).  Two gloo ranks play
-    ranks 6..7; their shard ids equal the single-batch ids of the same generations, and their
-    repairs / decode outcomes equal the oracle's over the whole-batch ids."""
+    """Config 4 (k=128 r=32, 65536 generations over 8 GPUs), shard ids only: ranks 6 and 7 own
+    the generations whose rid * sid products exceed 2^32 (galois_field.hh:143-158 wraps them).  Two
+    gloo ranks play ranks 6..7 and check that generation_shard gives them the single-batch ids of
+    the same generations and that the gloo max-reduce works; the repairs / outcomes compared here
+    are the oracle's on both sides (no engine runs -- the HIP engine on these ids is
+    test_gpu_multirank.py / test_gpu_parity.py's wrap cases)."""
     import torch.multiprocessing as mp
     from helpers import loss_exact_m, make_sources
     from netcode_amd.shard import generation_shard

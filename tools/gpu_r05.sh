@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-5 GPU steps, one parametrised script (replaces the one-off gpu_r04*.sh launchers).
+# usage: bash tools/gpu_r05.sh <tag> <step>[,<step>...] [bench args...]
+#   steps: tests (pytest -m gpu), dense (test_gpu_dense.py only), mb (tools/mb_issue),
+#          bench (default bench line), c2|c4|c5 (per-config lines), smoke
+set -o pipefail
+TAG=$1; STEPS=$2; shift 2
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+run() { local name=$1 t=$2; shift 2; echo "[$name] $*"; timeout -k 10 $t "$@" > $OUT/$name.log 2>&1; local rc=$?;
+        tail -3 $OUT/$name.log; [ $rc -eq 0 ] || { echo "[$name] rc=$rc"; exit $rc; }; }
+IFS=, read -ra S <<< "$STEPS"
+for s in "${S[@]}"; do
+  case $s in
+    tests) run pytest 900 python -u -m pytest tests -x -q -m gpu --timeout 240 --timeout-method thread ;;
+    dense) run dense 300 python -u -m pytest tests/test_gpu_dense.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
+    mb) run mb_issue 300 tools/mb_issue ;;
+    mbmix) run mb_mix 300 tools/mb_mix ;;
+    bench) run bench 300 python bench.py "$@" ;;
+    c2) run bench_c2 300 python bench.py --config k32r8s1024 "$@" ;;
+    c4) run bench_c4 300 python bench.py --config k128r32s1500 "$@" ;;
+    c5) run bench_c5 300 python bench.py --config k1024dense "$@" ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    ab) run ab_lib 900 bash tools/ab_lib.sh "$AB_OTHER" "$@" ;;
+    parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_shapes.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

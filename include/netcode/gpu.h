@@ -68,9 +68,12 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
 
 /* Region-MAC formulation (tuning and A/B testing; results are identical).  AUTO picks the
  * bit-sliced XOR kernel when the stride fills >= 1/3 of its 2 KiB wave span (stride % 16 == 0),
- * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice environment variable overrides
- * AUTO process-wide. */
-enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2 };
+ * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice|grouped environment variable
+ * overrides AUTO process-wide.  BITSLICE runs one independent wave per row tile (gf_mac_bs);
+ * BITSLICE_GROUPED (experimental, slower on MI355X: DESIGN.md §3) runs pairs of 16-row tiles per
+ * workgroup that build each source's bit planes once and share them through LDS (gf_mac_bsg). */
+enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2,
+       NTC_GF256_MAC_BITSLICE_GROUPED = 3 };
 int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);
 
 /* Decode-plan kernel (coverage and A/B testing; results are identical).  AUTO: the register-

@@ -36,6 +36,7 @@ struct ntc_gf256_engine {
   void* row_ptr = nullptr;     // bit-sliced decode: input row address per plan position
   size_t row_ptr_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;
+  uint32_t rowtile_force = 0;  // bit-sliced row tile 8 or 16 (NTC_GF256_ROWTILE; 0 = by rows)
   int plan_kind = NTC_GF256_PLAN_AUTO;
   // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
   bool timing = false;

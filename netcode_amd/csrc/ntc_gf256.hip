@@ -394,12 +394,16 @@ struct TMasks {
   uint32_t s4, s2, s1;                     // shift amounts 4, 2, 1
 };
 
+template <bool VSH = true>
 __device__ __forceinline__ TMasks tmasks()
 {
   TMasks t;
-  asm volatile("v_mov_b32 %0, 0x0f0f0f0f\n\tv_mov_b32 %1, 0x33333333\n\tv_mov_b32 %2, 0x55555555\n\t"
-               "v_mov_b32 %3, 4\n\tv_mov_b32 %4, 2\n\tv_mov_b32 %5, 1"
-               : "=v"(t.m4), "=v"(t.m2), "=v"(t.m1), "=v"(t.s4), "=v"(t.s2), "=v"(t.s1));
+  asm volatile("v_mov_b32 %0, 0x0f0f0f0f\n\tv_mov_b32 %1, 0x33333333\n\tv_mov_b32 %2, 0x55555555"
+               : "=v"(t.m4), "=v"(t.m2), "=v"(t.m1));
+  if constexpr (VSH)
+    asm volatile("v_mov_b32 %0, 4\n\tv_mov_b32 %1, 2\n\tv_mov_b32 %2, 1" : "=v"(t.s4), "=v"(t.s2), "=v"(t.s1));
+  else
+    t.s4 = 4, t.s2 = 2, t.s1 = 1;
   return t;
 }
 
@@ -412,17 +416,18 @@ __device__ __forceinline__ void swap_m(uint32_t& a, uint32_t& b, uint32_t sh, ui
   b = nb;
 }
 
+template <bool VSH = true>
 __device__ __forceinline__ void transpose8(uint32_t* d, const TMasks& t)
 {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) swap_m(d[i], d[i + 4], t.s4, t.m4);
+  for (int i = 0; i < 4; ++i) swap_m(d[i], d[i + 4], VSH ? t.s4 : 4u, t.m4);
 #pragma unroll
   for (int i = 0; i < 8; i += 4) {
-    swap_m(d[i], d[i + 2], t.s2, t.m2);
-    swap_m(d[i + 1], d[i + 3], t.s2, t.m2);
+    swap_m(d[i], d[i + 2], VSH ? t.s2 : 2u, t.m2);
+    swap_m(d[i + 1], d[i + 3], VSH ? t.s2 : 2u, t.m2);
   }
 #pragma unroll
-  for (int i = 0; i < 8; i += 2) swap_m(d[i], d[i + 1], t.s1, t.m1);
+  for (int i = 0; i < 8; i += 2) swap_m(d[i], d[i + 1], VSH ? t.s1 : 1u, t.m1);
 }
 
 __device__ __forceinline__ void transpose8(uint32_t* d)
@@ -596,14 +601,21 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       }
 #pragma unroll
       for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
+#ifndef NTC_ABL_NOFILL     // timing-only ablation builds (tools/build_variant.sh -DNTC_ABL_...)
       transpose8(Y);
+#endif
       if constexpr (!kLate) {
         vm_wait<2 * (kBsRing - 3)>();                  // source i+1 has landed
         lds_row((u + 1) % kBsRing, ycur);
       }
       jp += (i + 1 < k) ? jstep : 0u;
       on = const_load<CoefV>(jp);
+#ifndef NTC_ABL_NOFILL
       NTC_BS_TABLES(Y)
+#else
+#pragma unroll
+      for (int p = 8; p < kBsPlanes; ++p) Y[p] = ycur[p & 7];
+#endif
       uint64_t P0 = (static_cast<uint64_t>(o[1]) << 32) | o[0];
       const uint32_t slot = slotm[(u + kBsRing - 1) % kBsRing];
       // the DMA's biased row base, formed here (the scalar load of the row address was issued an
@@ -613,9 +625,13 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       const uint8_t* row2 = PAIR ? row + poff_in : row;   // the second piece's row (pairing)
       const uint8_t* nrow_next = DEC ? row_at(i + kBsRing) : nrow + ((i + kBsRing < k) ? stride : 0u);
       // refill the slot of source i-1 with source i+3, then the chain (one M0 save / restore)
+#ifndef NTC_ABL_NODMA
 #define NTC_BS_DMA_FULL \
       "s_mov_b32 s94, m0\n" "s_mov_b32 m0, %[slot]\n" "s_nop 0\n" \
       "global_load_lds_dwordx4 %[x], %[row]\n" "global_load_lds_dwordx4 %[x], %[row] offset:1024\n"
+#else                      // timing-only ablation: the ring keeps whatever it holds
+#define NTC_BS_DMA_FULL "s_mov_b32 s94, m0\n"
+#endif
 #define NTC_BS_DMA_PART \
       "s_mov_b32 s94, m0\n" "s_mov_b32 m0, %[slot]\n" "s_nop 0\n" \
       "global_load_lds_dwordx4 %[d0], %[row]\n" "s_add_u32 m0, %[slot], 0x400\n" "s_nop 0\n" \
@@ -625,40 +641,41 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       "s_lshl_b32 s98, s90, 24\n" "s_lshr_b32 s98, s98, 17\n" \
       "s_add_u32 s98, s96, s98\n" "s_addc_u32 s99, s97, 0\n" \
       "s_swappc_b64 s[92:93], s[98:99]\n"
-#define NTC_BS_SECOND \
-      "s_mov_b64 s[90:91], %[p1]\n" "s_cmp_eq_u64 s[90:91], 0\n" "s_cbranch_scc1 LBS2%=\n" \
-      "s_set_gpr_idx_idx 64\n" \
-      "s_lshl_b32 s98, s90, 24\n" "s_lshr_b32 s98, s98, 17\n" \
-      "s_add_u32 s98, s96, s98\n" "s_addc_u32 s99, s97, 0\n" \
-      "s_swappc_b64 s[92:93], s[98:99]\n" "LBS2%=:\n"
+#ifdef NTC_ABL_NOCHAIN
+#undef NTC_BS_ENTER
+#define NTC_BS_ENTER ""
+#define NTC_BS_LEAVE "s_mov_b32 m0, s94\n"
+#else
 #define NTC_BS_LEAVE "s_set_gpr_idx_off\n" "s_mov_b32 m0, s94\n"
+#endif
 #define NTC_BS_CLOB "s92", "s93", "s94", "s98", "s99", "scc", "memory"
       if constexpr (R == 8) {
+        uint64_t Z = 0;                                // no second half (s[88:89], the table's stub)
         if constexpr (FULL)
           asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_LEAVE
-                       : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
+                       : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0), [q] "+{s[88:89]}"(Z)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [x] "v"(x),
                          [row] "s"(row)
                        : NTC_BS_CLOB);
         else
           asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_LEAVE
-                       : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0)
+                       : NTC_BS_OUTS8(A), [p] "+{s[90:91]}"(P0), [q] "+{s[88:89]}"(Z)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
                          [d1] "v"(d1), [row] "s"(row), [row2] "s"(row2)
                        : NTC_BS_CLOB);
       } else {
-        const uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];
+        uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];     // rows 8-15: s[88:89]
         if constexpr (FULL)
-          asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
-                       : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
+          asm volatile(NTC_BS_DMA_FULL NTC_BS_ENTER NTC_BS_LEAVE
+                       : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0), [q] "+{s[88:89]}"(P1)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [x] "v"(x),
-                         [row] "s"(row), [p1] "s"(P1)
+                         [row] "s"(row)
                        : NTC_BS_CLOB);
         else
-          asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_SECOND NTC_BS_LEAVE
-                       : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0)
+          asm volatile(NTC_BS_DMA_PART NTC_BS_ENTER NTC_BS_LEAVE
+                       : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0), [q] "+{s[88:89]}"(P1)
                        : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase), [slot] "s"(slot), [d0] "v"(d0),
-                         [d1] "v"(d1), [row] "s"(row), [row2] "s"(row2), [p1] "s"(P1)
+                         [d1] "v"(d1), [row] "s"(row), [row2] "s"(row2)
                        : NTC_BS_CLOB);
       }
       nrow = nrow_next;
@@ -737,6 +754,221 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
   } else {
     bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring);
   }
+}
+
+// ---- grouped bit-sliced MAC: NT row tiles of one (generation, span) share the source fill ----
+// The per-source fill -- the 8x8 bit transpose and the 22 plane-table XORs, 70+ VALU -- depends
+// only on the source, not on the row tile, yet every 16-row tile of a generation repeated it.
+// Here a workgroup holds the NT tiles of one (generation, 2 KiB column span): source i's 30 table
+// planes are built ONCE, by wave i % NT, and published in LDS; every wave reads them (8 b128
+// reads) and runs its own tile's chain.  Per source step:
+//   read planes(i) from table slot i % 2 -> chain(i) -> [wave (i+1) % NT: build planes(i+1) into
+//   slot (i+1) % 2] -> barrier
+// Slot i % 2 is rewritten (with source i+2) only after the barrier that ends step i, when every
+// wave has read it.  Each wave streams ITS OWN sources (s % NT == w) through a private ring of 2
+// LDS slots by LDS-DMA, issued 2 * NT sources ahead, so no barrier guards the raw bytes.
+// A wave whose tile has no rows (a decode generation with fewer rows than the group) still builds
+// its share of the planes.
+constexpr uint32_t kTabSlot = 8u * 1024u;   // 32 planes (30 used) x 64 lanes x 4 B, [quad][lane][4]
+constexpr int kGrpRaw = 2;                  // raw-source slots per wave
+
+template <int NT, bool DEC, bool FULL>
+__device__ __forceinline__ void bs_group(const MacArgs& a, uint32_t g, uint32_t tile, uint32_t nrows,
+                                         uint32_t cc, uint32_t lane, uint32_t w, uint32_t ring,
+                                         uint32_t tabs, uint32_t i_begin, uint32_t i_count,
+                                         uint32_t steps, bool idle, uint8_t* out_base)
+{
+  const size_t stride = a.stride;
+  const uint32_t k = idle ? 0u : i_count;              // sources this group sums (<= steps)
+  const uint32_t col = cc * 2048u;
+  const uint32_t x = ring + lane * 16u;                 // LDS read offset of this lane's piece 0
+  const bool v0 = FULL || col + lane * 16u < stride;
+  const bool v1 = FULL || col + lane * 16u + 1024u < stride;
+  const uint32_t d0 = v0 ? x : ring, d1 = v1 ? x + 1024u : ring;   // !FULL DMA offsets (clamped)
+  const uint8_t* base0 = a.in0 + (static_cast<size_t>(g) * a.k + i_begin) * stride;
+  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (a.k + kBsRing) : nullptr;
+  const uint8_t* jp = a.coef + (static_cast<size_t>(g) * a.k + i_begin) * a.rp + tile * 16u;
+  const uint64_t bias = static_cast<uint64_t>(col) - ring;
+  const bool has_rows = nrows != 0;
+  auto row_at = [&](uint32_t i) -> const uint8_t* {    // scalar row address of source i
+    uint64_t v;
+    if constexpr (DEC) v = const_load<uint64_t>(rowp + i);
+    else v = reinterpret_cast<uint64_t>(base0 + static_cast<size_t>(i) * stride);
+    const uint32_t lo = uniform(static_cast<uint32_t>(v)), hi = uniform(static_cast<uint32_t>(v >> 32));
+    return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  // raw slot of source s (this wave's s-th own source, s % NT == w): (s / NT) % 2
+  auto dma = [&](uint32_t s) {
+    const uint8_t* row = row_at(s) + bias;
+    const uint32_t slot = uniform(ring + ((s / NT) & 1u) * kBsSlot);
+    uint32_t keep;
+    if constexpr (FULL)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, %2\n\t"
+                   "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(x), "s"(row), "s"(slot) : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, %3\n\t"
+                   "s_add_u32 m0, %4, 0x400\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %2, %3\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(d0), "v"(d1), "s"(row), "s"(slot) : "memory", "scc");
+  };
+#ifndef NTC_GRP_VSH
+#define NTC_GRP_VSH 0
+#endif
+  const TMasks tm = tmasks<NTC_GRP_VSH>();
+  // build source s's planes (s % NT == w) from its raw slot into table slot s % 2
+  auto produce = [&](uint32_t s) {
+    if (s + NT < k) vm_wait<2>();                      // source s + NT is the younger DMA in flight
+    else vm_wait<0>();
+    const uint32_t slot = ((s / NT) & 1u) * kBsSlot;
+    uint32_t Y[kBsPlanes];
+    {
+      const auto* p = reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(x + slot);
+      const u32x4 q0 = p[0], q1 = p[1024 / 16];
+      Y[0] = q0[0]; Y[1] = q0[1]; Y[2] = q0[2]; Y[3] = q0[3];
+      Y[4] = q1[0]; Y[5] = q1[1]; Y[6] = q1[2]; Y[7] = q1[3];
+    }
+    // the slot's bytes are in registers once this wave's LDS reads return: refill it with the
+    // wave's source two rounds on (the DMA writes LDS behind the reads, in issue order)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Y[0]), "+v"(Y[1]), "+v"(Y[2]), "+v"(Y[3]), "+v"(Y[4]),
+                 "+v"(Y[5]), "+v"(Y[6]), "+v"(Y[7]) :: "memory");
+    if (s + 2 * NT < k) dma(s + 2 * NT);
+    transpose8<NTC_GRP_VSH>(Y, tm);
+    // planes published quad by quad as they are formed (NTC_BS_TABLES' order), so at most the
+    // 8 input planes and one quad of combinations are live beside the accumulators
+    auto* t = reinterpret_cast<__attribute__((address_space(3))) u32x4*>(tabs + (s & 1u) * kTabSlot + lane * 16u);
+    t[0] = u32x4{Y[0], Y[1], Y[2], Y[3]};
+    t[64] = u32x4{Y[4], Y[5], Y[6], Y[7]};
+    Y[8] = Y[1] ^ Y[0]; Y[9] = Y[2] ^ Y[0]; Y[10] = Y[2] ^ Y[1]; Y[11] = Y[10] ^ Y[0];
+    t[2 * 64] = u32x4{Y[8], Y[9], Y[10], Y[11]};
+    Y[12] = Y[3] ^ Y[0]; Y[13] = Y[3] ^ Y[1]; Y[14] = Y[13] ^ Y[0]; Y[15] = Y[3] ^ Y[2];
+    t[3 * 64] = u32x4{Y[12], Y[13], Y[14], Y[15]};
+    Y[16] = Y[15] ^ Y[0]; Y[17] = Y[15] ^ Y[1]; Y[18] = Y[17] ^ Y[0]; Y[19] = Y[5] ^ Y[4];
+    t[4 * 64] = u32x4{Y[16], Y[17], Y[18], Y[19]};
+    Y[20] = Y[6] ^ Y[4]; Y[21] = Y[6] ^ Y[5]; Y[22] = Y[21] ^ Y[4]; Y[23] = Y[7] ^ Y[4];
+    t[5 * 64] = u32x4{Y[20], Y[21], Y[22], Y[23]};
+    Y[24] = Y[7] ^ Y[5]; Y[25] = Y[24] ^ Y[4]; Y[26] = Y[7] ^ Y[6]; Y[27] = Y[26] ^ Y[4];
+    t[6 * 64] = u32x4{Y[24], Y[25], Y[26], Y[27]};
+    Y[28] = Y[26] ^ Y[5]; Y[29] = Y[28] ^ Y[4];
+    *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(&t[7 * 64]) = u32x2{Y[28], Y[29]};
+  };
+  static_assert(kBsPlanes == 30, "bs_group publishes the 30 planes of NTC_BS_TABLES");
+
+  u32x8 A[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t tbase = bs_table_base();
+  // prologue: this wave's first two own sources in flight; wave 0 builds source 0
+  if (w < k) dma(w);
+  if (w + NT < k) dma(w + NT);
+  if (w == 0 && k) produce(0);
+  __syncthreads();
+  u32x4 on = has_rows && k ? const_load<u32x4>(jp) : u32x4{0, 0, 0, 0};
+  for (uint32_t i = 0; i < steps; ++i) {
+    if (has_rows && i < k) {
+      const u32x4 o = on;
+      jp += a.rp;
+      if (i + 1 < k) on = const_load<u32x4>(jp);
+      uint32_t Y[kBsPlanes];
+      {
+        const auto* t = reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(
+            tabs + (i & 1u) * kTabSlot + lane * 16u);
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+          const u32x4 v = t[q * 64];
+          Y[4 * q] = v[0]; Y[4 * q + 1] = v[1]; Y[4 * q + 2] = v[2]; Y[4 * q + 3] = v[3];
+        }
+        const u32x2 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x2*>(&t[7 * 64]);
+        Y[28] = v[0];
+        Y[29] = v[1];
+      }
+      uint64_t P0 = (static_cast<uint64_t>(o[1]) << 32) | o[0];
+      uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];           // rows 8-15: s[88:89]
+      asm volatile("s_mov_b32 s94, m0\n" NTC_BS_ENTER NTC_BS_LEAVE
+                   : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0), [q] "+{s[88:89]}"(P1)
+                   : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase)
+                   : NTC_BS_CLOB);
+    }
+    if (i + 1 < k && (i + 1) % NT == w) produce(i + 1);
+    __syncthreads();
+  }
+
+  if (idle) return;
+  const uint32_t row0 = tile * 16u;
+  const uint32_t c0 = col + lane * 16u, c1 = c0 + 1024u;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (static_cast<uint32_t>(j) >= nrows) continue;
+    uint32_t acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = A[j][p];
+    transpose8<NTC_GRP_VSH>(acc, tm);
+    uint8_t* dst;
+    if constexpr (DEC) {
+      const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
+      dst = a.out + static_cast<size_t>(g) * a.k * stride + uniform(outs[j]) * stride;
+    } else {
+      dst = out_base + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
+    }
+    if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+    if (v1) *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+// One workgroup of GPB groups of NT waves; group = (generation, NT 16-row tiles, 2 KiB column
+// span[, split-k part]); blocks renumbered per XCD as in gf_mac_bs.  Four-wave workgroups (GPB =
+// 2 pairs) are dispatched one wave per SIMD, like gf_mac_bs's; the groups share only the barrier.
+template <int NT, bool DEC, bool FULL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void gf_mac_bsg(MacArgs a)
+{
+  constexpr uint32_t GPB = 4 / NT;
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[GPB * NT * kGrpRaw * kBsSlot];
+  __shared__ __attribute__((aligned(16))) uint8_t s_tab[GPB * 2 * kTabSlot];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wid = uniform(threadIdx.x >> 6);
+  const uint32_t gi = wid / NT, w = wid % NT;          // group in the block, wave in the group
+  const uint32_t nb = gridDim.x;                       // a multiple of 8 (launch_mac)
+  uint32_t task = ((blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3)) * GPB + gi;
+  task = uniform(task);
+  uint32_t cc, grp;
+  const uint32_t ngrp = (a.nrowchunks + NT - 1) / NT;
+  if (a.tile_fast) {
+    grp = task % ngrp;
+    task /= ngrp;
+    cc = task % a.ncolchunks;
+    task /= a.ncolchunks;
+  } else {
+    cc = task % a.ncolchunks;
+    task /= a.ncolchunks;
+    grp = task % ngrp;
+    task /= ngrp;
+  }
+  uint32_t ks = 0;
+  if (!DEC && a.ksplit > 1) {
+    ks = task % a.ksplit;
+    task /= a.ksplit;
+  }
+  const uint32_t g = task;
+  // a group with nothing to do still takes part in the block's barriers (the other group's
+  // steps): it runs k steps with no rows and builds nothing -- see bs_group's `idle`
+  const uint32_t total = g < a.G ? (DEC ? uniform(a.rows_per_gen[g]) : a.rows) : 0u;
+  const bool idle = grp * NT * 16u >= total;           // uniform over the group
+  const uint32_t tile = grp * NT + w;
+  const uint32_t row0 = tile * 16u;
+  const uint32_t nrows = row0 < total ? min(16u, total - row0) : 0u;
+  const uint32_t ring = lds_addr(s_raw + (gi * NT + w) * (kGrpRaw * kBsSlot));
+  const uint32_t tabs = lds_addr(s_tab + gi * 2 * kTabSlot);
+  const uint32_t i0 = ks * a.kpart;
+  const uint32_t cnt = a.ksplit > 1 ? min(a.kpart, a.k - i0) : a.k;
+  // every group of the block runs the same number of steps (a split-k part of another group may
+  // be shorter: the block runs the longest part, shorter groups idle through the tail steps)
+  const uint32_t steps = a.ksplit > 1 ? a.kpart : a.k;
+  bs_group<NT, DEC, FULL>(a, idle ? 0u : g, tile, idle ? 0u : nrows, cc, lane, w, ring, tabs, i0, cnt,
+                          steps, idle, ks ? a.kout + (ks - 1) * a.kout_step : a.out);
 }
 
 // Input row address of every plan position for the bit-sliced decode MAC: position i < k reads
@@ -2299,7 +2531,8 @@ mac_fn pick_kernel(bool dec, int D)
 bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
 {
   if (stride % 16 != 0) return false;
-  if (e->mac_kind != NTC_GF256_MAC_AUTO) return e->mac_kind == NTC_GF256_MAC_BITSLICE;
+  if (e->mac_kind != NTC_GF256_MAC_AUTO)
+    return e->mac_kind == NTC_GF256_MAC_BITSLICE || e->mac_kind == NTC_GF256_MAC_BITSLICE_GROUPED;
   const uint32_t pieces = stride / 16, spans = (stride + 2047) / 2048;   // 16-B pieces per span: 128
   return pieces * 100 >= spans * 128 * 33;
 }
@@ -2313,6 +2546,12 @@ mac_fn pick_bs(bool dec, uint32_t rowtile, bool full, bool pair)
                : (full ? gf_mac_bs<16, false, true> : gf_mac_bs<16, false, false>);
   return dec ? (full ? gf_mac_bs<8, true, true> : gf_mac_bs<8, true, false>)
              : (full ? gf_mac_bs<8, false, true> : gf_mac_bs<8, false, false>);
+}
+
+mac_fn pick_bsg(bool dec, bool full)
+{
+  return dec ? (full ? gf_mac_bsg<2, true, true> : gf_mac_bsg<2, true, false>)
+             : (full ? gf_mac_bsg<2, false, true> : gf_mac_bsg<2, false, false>);
 }
 
 // out ^= the split-k parts 1 .. nparts (16 B per thread and step, grid-stride)
@@ -2336,14 +2575,19 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   mac_fn fn;
   uint32_t rowtile, span, wpb;
   uint64_t blk_align = 1;
+  uint32_t group = 1;                           // 16-row tiles per workgroup sharing the fill
   if (a.pair || use_bitslice(e, a.stride)) {
     // 16-row tiles (3 waves per SIMD) once a tile has more than 8 rows to fill, else 8-row
     // tiles (4 waves per SIMD)
-    rowtile = a.rows > 8 ? 16u : 8u;
+    rowtile = e->rowtile_force ? e->rowtile_force : a.rows > 8 ? 16u : 8u;
     span = 2048;
     wpb = kBsWaves;
     blk_align = 8;                              // the kernel's XCD renumbering
     fn = pick_bs(dec, rowtile, a.stride % 2048 == 0, a.pair != nullptr);
+    if (!a.pair && rowtile == 16 && e->mac_kind == NTC_GF256_MAC_BITSLICE_GROUPED && a.rows > 16) {
+      group = 2;                                // gf_mac_bsg: tile pairs share the source fill
+      fn = pick_bsg(dec, a.stride % 2048 == 0);
+    }
     if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBsRing);
       int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
@@ -2414,13 +2658,17 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     a.kout = static_cast<uint8_t*>(e->kout);
     tasks *= a.ksplit;
   }
+  if (group > 1) {                              // 4-wave workgroups of 4 / group tile groups
+    tasks = tasks / a.nrowchunks * ((a.nrowchunks + group - 1) / group);
+    wpb = 4 / group;
+  }
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
   {
     KernelTimer kt(e, dec ? NTC_GF256_K_DECODE_MAC : NTC_GF256_K_ENCODE_MAC, st, true);
-    hipExtLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(64 * wpb), 0, st, kt.start(),
-                          kt.stop(), 0, a);
+    hipExtLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(group > 1 ? 256 : 64 * wpb), 0,
+                          st, kt.start(), kt.stop(), 0, a);
   }
   int rc = hip_check(hipGetLastError(), what);
   if (!rc && a.ksplit > 1) {
@@ -2537,6 +2785,21 @@ int ntc_gf256_engine_create(int device, ntc_gf256_engine** out)
   auto* e = new (std::nothrow) ntc_gf256_engine;
   if (!e) return fail(NTC_GPU_ENOMEM, "host allocation");
   e->device = device;
+  // process-wide overrides of the AUTO choices (gpu.h): A/B runs without a rebuild
+  if (const char* m = std::getenv("NTC_GF256_MAC")) {
+    if (!std::strcmp(m, "perm")) e->mac_kind = NTC_GF256_MAC_PERM;
+    else if (!std::strcmp(m, "bitslice")) e->mac_kind = NTC_GF256_MAC_BITSLICE;
+    else if (!std::strcmp(m, "grouped")) e->mac_kind = NTC_GF256_MAC_BITSLICE_GROUPED;
+  }
+  if (const char* t = std::getenv("NTC_GF256_ROWTILE")) {
+    if (!std::strcmp(t, "8")) e->rowtile_force = 8;
+    else if (!std::strcmp(t, "16")) e->rowtile_force = 16;
+  }
+  if (const char* p = std::getenv("NTC_GF256_PLAN")) {
+    if (!std::strcmp(p, "wave")) e->plan_kind = NTC_GF256_PLAN_WAVE;
+    else if (!std::strcmp(p, "lds")) e->plan_kind = NTC_GF256_PLAN_LDS;
+    else if (!std::strcmp(p, "big")) e->plan_kind = NTC_GF256_PLAN_BIG;
+  }
   *out = e;
   return NTC_GPU_OK;
 }
@@ -2589,7 +2852,7 @@ int ntc_gf256_mac_time(ntc_gf256_engine* e, int dec, float* ms)
 int ntc_gf256_set_mac_kind(ntc_gf256_engine* e, int kind)
 {
   if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
-  if (kind < NTC_GF256_MAC_AUTO || kind > NTC_GF256_MAC_BITSLICE) return fail(NTC_GPU_EINVAL, "unknown MAC kind");
+  if (kind < NTC_GF256_MAC_AUTO || kind > NTC_GF256_MAC_BITSLICE_GROUPED) return fail(NTC_GPU_EINVAL, "unknown MAC kind");
   e->mac_kind = kind;
   return NTC_GPU_OK;
 }

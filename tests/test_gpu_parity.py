@@ -50,7 +50,7 @@ def gpu_decode(d, lost, llen, smask, rep, rsz, rmask, sid=None, rid=None):
     return host(s_t), host(l_t, np.uint16), status_to_numpy(st)
 
 
-@pytest.fixture(params=["auto", "perm", "bitslice"])
+@pytest.fixture(params=["auto", "perm", "bitslice", "grouped"])
 def mac(request, gpu):
     """Run a parity test under each region-MAC formulation (ntc_gf256_set_mac_kind)."""
     from netcode_amd.engine import Engine
@@ -111,6 +111,12 @@ ENCODE_CASES = [
     # second ragged); uint32-wrapping ids and unequal lengths (one size product per source)
     (3, 37, 300, 1024, 1024, True, "wrap"),
     (2, 64, 513, 512, 512, False, "offset"),
+    # tile-pair workgroups (gf_mac_bsg, > 16 rows): k below the group size (wave 1 builds no
+    # source, or one), partial spans with a short k, a second group with one idle wave
+    (4, 1, 24, 2048, 2048, True, "offset"),
+    (3, 2, 17, 4096, 4096, False, "default"),
+    (3, 3, 40, 4112, 4112, True, "offset"),
+    (2, 5, 33, 2080, 2080, True, "wrap"),
 ]
 
 
@@ -171,6 +177,10 @@ DECODE_CASES = [
     # candidate repair fails (decoder.cc:448-468 retry; the LDS plan's rank screening)
     (400, 100, 64, 64, 64, "iid", 0.35, False),
     (400, 60, 40, 64, 64, "iid", 0.3, True),
+    # tile-pair workgroups (gf_mac_bsg): m ~ U[0, 20] (some pairs with an idle second wave, some
+    # generations with nothing to decode), and 3 row tiles over a partial span
+    (16, 24, 20, 2048, 2048, "mixed", 20, True),
+    (10, 40, 36, 4112, 4112, "exact", 36, False),
 ]
 
 

@@ -21,7 +21,8 @@ kernel shares it and its loop stays short.
 
 Registers fixed by the table: Y[0..29] in v2..v31, accumulators v32.. (8-row tiles v32..v95,
 16-row tiles v32..v159: <= 168 VGPRs, 3 waves per SIMD), s[90:91] coefficient bytes, s[92:93]
-return address, s[96:97] table base, s98/s99 scratch, M0 the row index.
+return address, s[88:89] the second half's coefficient bytes of a 16-row tile (0: none),
+s[96:97] table base, s98/s99 scratch, M0 the row index.
 
 Usage: python tools/gen_bitslice_table.py   (rewrites the .inc; commit the result)
 """
@@ -99,7 +100,14 @@ def table(safe):
         lines += block_ops(c) + tail
         # pad to exactly BLOCK bytes: an encoding that grew is an assembler error, not a misjump
         lines.append(f".fill {BLOCK} - (. - {lab}), 1, 0")
-    lines += [f"ntc_bs_ret_{tag}:", "s_setpc_b64 s[92:93]"]
+    # end of a row run: a 16-row tile's second half (its 8 coefficient bytes in s[88:89], zero
+    # for none) continues at row 8 in the same call -- one return and one call fewer per source
+    lines += [f"ntc_bs_ret_{tag}:", "s_cmp_eq_u64 s[88:89], 0", f"s_cbranch_scc1 ntc_bs_out_{tag}",
+              "s_mov_b64 s[90:91], s[88:89]", "s_mov_b64 s[88:89], 0", "s_set_gpr_idx_idx 64",
+              "s_lshl_b32 s98, s90, 24", "s_lshr_b32 s98, s98, 17", "s_add_u32 s98, s96, s98"]
+    if safe:
+        lines.append("s_addc_u32 s99, s97, 0")
+    lines += ["s_setpc_b64 s[98:99]", f"ntc_bs_out_{tag}:", "s_setpc_b64 s[92:93]"]
     return lines
 
 

@@ -21,6 +21,8 @@ for s in "${S[@]}"; do
     c5) run bench_c5 300 python bench.py --config k1024dense "$@" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     ab) run ab_lib 900 bash tools/ab_lib.sh "$AB_OTHER" "$@" ;;
+    abenv) run ab_env 900 bash tools/ab_env.sh "$AB_A" "$AB_B" "$@" ;;
+    abl) eval "run abl 900 bash tools/abl_run.sh $ABL -- $*" ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_shapes.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -36,8 +36,13 @@ size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT N
  * once, inside the call that produced it: callbacks then run both there and at the flush, so a
  * handler must be re-entrant with respect to the objects of the same batch.  Events that handlers
  * produce during a flush (e.g. a decoder fed from an encoder's packet handler) are queued for the
- * next flush: flush until ntc_batch_pending is 0 to drain such chains.  Attaching an object
- * to another batch or to NULL flushes its current batch first.
+ * next flush: flush until ntc_batch_pending is 0 to drain such chains.  Asynchronous mode
+ * (ntc_batch_set_async, off by default): ntc_batch_flush first delivers the events of the
+ * previous flush, then starts the device work of the queued ones and returns without waiting;
+ * those are delivered by the next ntc_batch_flush, so one flush's GPU round trip overlaps the
+ * caller's work until the next (ntc_batch_pending counts them; flush until it is 0 to drain).
+ * Each object's callback sequence is unchanged; objects with events in flight queue new ones
+ * behind them.  Attaching an object to another batch or to NULL drains its current batch first.
  * Deleting an attached object discards its queued events; deleting a batch discards every queued
  * event and detaches its objects. */
 typedef struct ntc_batch_t ntc_batch_t;
@@ -48,6 +53,7 @@ void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* batch, ntc_error* er
 void ntc_batch_flush(ntc_batch_t* batch, ntc_error* error) NTC_C_NOEXCEPT NTC_C_NONNULL;
 size_t ntc_batch_pending(const ntc_batch_t* batch) NTC_C_NOEXCEPT NTC_C_NONNULL;
 void ntc_batch_set_eager(ntc_batch_t* batch, int on) NTC_C_NOEXCEPT;   /* NULL is a no-op */
+void ntc_batch_set_async(ntc_batch_t* batch, int on) NTC_C_NOEXCEPT;   /* NULL is a no-op */
 
 /* GF(2^w) region work on host buffers, run on the MI355X engine (one H2D, one combine launch,
  * one D2H): the region operations of the C++ detail layer (include/netcode/detail/galois_field.hh,

@@ -84,6 +84,7 @@ def load():
         "ntc_encoder_set_batch": (None, [P, P, E]), "ntc_decoder_set_batch": (None, [P, P, E]),
         "ntc_batch_flush": (None, [P, E]),
         "ntc_batch_pending": (S, [P]), "ntc_batch_set_eager": (None, [P, C.c_int]),
+        "ntc_batch_set_async": (None, [P, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -198,13 +199,15 @@ class Batch:
     """ntc_batch_t (netcode/c/ext.h): attached encoders' packets are queued until flush(), which
     computes every pending repair in one GPU launch per field size and emits in production order."""
 
-    def __init__(self, eager: bool = False):
+    def __init__(self, eager: bool = False, asynchronous: bool = False):
         self.L = load()
         self.h = self.L.ntc_new_batch()
         if not self.h:
             raise MemoryError
         if eager:
             self.L.ntc_batch_set_eager(self.h, 1)
+        if asynchronous:          # a flush delivers the previous flush's events, returns at once
+            self.L.ntc_batch_set_async(self.h, 1)
 
     def flush(self):
         err = Error(0, None)

@@ -84,7 +84,7 @@ using Expr = std::vector<Term>;
 
 // A payload: base (bytes handed in or received) or derived (a linear combination of other
 // payloads, evaluated at a batch flush after everything it reads).  Immutable once created.
-struct Node {
+struct Node : std::enable_shared_from_this<Node> {
   bytes host;                  // base: the payload (from byte hoff on); derived: its value once fetched
   uint32_t hoff = 0;           // a received packet's buffer is adopted whole: payload offset in it
   uint16_t size = 0;
@@ -249,9 +249,13 @@ class Device {
   // Batch flush: evaluate every derived node the roots need (each after the nodes it reads),
   // then bring the roots' values to the host.  GF(2^8): payloads on the device arena, one
   // gather_combine launch per dependency level; other fields: per level one host-staged combine.
-  void evaluate(const std::vector<Node*>& roots)
+  // async (ntc_batch_set_async): enqueue the GF(2^8) work and return; its results land in the
+  // nodes at the next complete() / evaluate() (other fields' work, host-staged, completes here).
+  // Any earlier asynchronous flush is completed first, so at most one is in flight.
+  void evaluate(const std::vector<Node*>& roots, bool async = false)
   {
     std::lock_guard<std::mutex> lock(mu_);
+    complete_locked();
     const uint64_t ep = ++epoch_;
     std::vector<Node*> todo;                       // dependencies first
     std::vector<std::pair<Node*, size_t>> stack;
@@ -282,7 +286,14 @@ class Device {
     std::vector<Node*> t8, tw;
     for (Node* n : todo) (n->w == 8 ? t8 : tw).push_back(n);
     if (!tw.empty()) evaluate_host(tw);
-    if (!t8.empty() || !roots.empty()) evaluate_w8(t8, roots, ep);
+    if (!t8.empty() || !roots.empty()) evaluate_w8(t8, roots, ep, async);
+  }
+
+  // the results of an asynchronous evaluate(): wait for its work, then values into the nodes
+  void complete()
+  {
+    std::lock_guard<std::mutex> lock(mu_);
+    complete_locked();
   }
 
  private:
@@ -347,7 +358,8 @@ class Device {
   // job / term descriptors go up in ONE copy into the flush's arena region; a root's result is
   // written by its job both into the arena and straight into pinned host memory (the job's second
   // output), so a flush is one copy, one launch per dependency level and one synchronisation.
-  void evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep)
+  void evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep,
+                   bool async = false)
   {
     const uint64_t up_mark = ep + (1ull << 63);
     std::vector<Node*> up;
@@ -429,6 +441,21 @@ class Device {
       check(hipMemcpyAsync(h_down_ + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
       lp += pad16(r->size);
     }
+    if (async) {
+      // in flight: the nodes count as resident for later launches (stream order), their host
+      // values and the staging are taken over by complete_locked(); the flight record keeps
+      // every node alive (an expression's terms hold its inputs' arena chunks) until then
+      check(hipEventRecord(done_, stream_), "hipEventRecord");
+      ++launches_;
+      flight_.on = true;
+      for (Node* n : todo) {
+        n->done = true;
+        flight_.todo.push_back(n->shared_from_this());
+      }
+      for (Node* r : roots)
+        if (r->derived && !r->fetched && r->rpos != kNoPos) flight_.roots.push_back(r->shared_from_this());
+      return;
+    }
     wait_stream();
 #else
     std::memset(h_down_, 0, root_bytes + late_bytes);
@@ -445,6 +472,40 @@ class Device {
     }
     for (Node* r : roots) {
       if (!r->derived || r->fetched || r->rpos == kNoPos) continue;
+      r->host.assign(h_down_ + r->rpos, h_down_ + r->rpos + r->size);
+      r->fetched = true;
+      r->rpos = kNoPos;
+    }
+  }
+
+  // the in-flight asynchronous flush (at most one): its work, then its nodes' values
+  struct Flight {
+    bool on = false;
+    std::vector<NodeRef> todo, roots;
+  };
+  Flight flight_;
+
+  void complete_locked()
+  {
+    if (!flight_.on) return;
+#ifndef NTC_CAPI_HOST_STUB
+    hipError_t e;
+    const auto t0 = std::chrono::steady_clock::now();
+    while ((e = hipEventQuery(done_)) == hipErrorNotReady)
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
+        e = hipEventSynchronize(done_);
+        break;
+      }
+    Flight f = std::move(flight_);
+    flight_ = Flight{};
+    check(e, "hipEventQuery");
+#else
+    Flight f = std::move(flight_);
+    flight_ = Flight{};
+#endif
+    for (const NodeRef& n : f.todo) n->expr.clear();
+    for (const NodeRef& r : f.roots) {
+      if (r->fetched || r->rpos == kNoPos) continue;
       r->host.assign(h_down_ + r->rpos, h_down_ + r->rpos + r->size);
       r->fetched = true;
       r->rpos = kNoPos;
@@ -1564,6 +1625,8 @@ class Batch {
     encs_.erase(std::remove(encs_.begin(), encs_.end(), e), encs_.end());
     q_.erase(std::remove_if(q_.begin(), q_.end(), [e](const Pending& p) { return p.enc == e; }),
              q_.end());
+    flight_q_.erase(std::remove_if(flight_q_.begin(), flight_q_.end(),
+                                   [e](const Pending& p) { return p.enc == e; }), flight_q_.end());
   }
   void detach(Decoder* d)
   {
@@ -1571,6 +1634,8 @@ class Batch {
     decs_.erase(std::remove(decs_.begin(), decs_.end(), d), decs_.end());
     q_.erase(std::remove_if(q_.begin(), q_.end(), [d](const Pending& p) { return p.dec == d; }),
              q_.end());
+    flight_q_.erase(std::remove_if(flight_q_.begin(), flight_q_.end(),
+                                   [d](const Pending& p) { return p.dec == d; }), flight_q_.end());
   }
   void push(Pending&& p) { q_.push_back(std::move(p)); }
   // a packet buffer of an already flushed event (empty, capacity kept), or a new one
@@ -1582,8 +1647,20 @@ class Batch {
     b.clear();
     return b;
   }
-  size_t pending() const { return q_.size(); }
+  size_t pending() const { return q_.size() + flight_q_.size(); }
   void flush();
+  void drain()                           // every queued and in-flight event delivered
+  {
+    const bool a = async;
+    async = false;
+    flush();
+    async = a;
+  }
+  // Asynchronous flushes (opt-in, ntc_batch_set_async): flush() delivers the previous flush's
+  // events, then starts the GPU work of the queued ones and returns; they are delivered by the
+  // next flush (flush until pending() is 0 to drain).  The device work of one flush overlaps
+  // whatever the caller does until the next.
+  bool async = false;
   // Eager emission (opt-in, ntc_batch_set_eager): an event that needs no GF result -- a source
   // packet, a received source's delivery, an ack -- of an object with nothing queued goes out at
   // once instead of at the flush.
@@ -1593,7 +1670,9 @@ class Batch {
   std::vector<Encoder*> encs_;
   std::vector<Decoder*> decs_;
   std::vector<Pending> q_;
+  std::vector<Pending> flight_q_;   // an asynchronous flush's events, awaiting its results
   std::vector<Pending> spare_;   // the last flushed queue's storage, reused by the next one
+  void emit(std::vector<Pending>& q);
   std::vector<bytes> pool_;      // flushed packets' buffers (no malloc / free per packet)
 };
 
@@ -1609,7 +1688,7 @@ void Encoder::set_batch(Batch* b)
 {
   if (b == batch_) return;
   if (batch_) {
-    batch_->flush();                    // keep this encoder's packet order across the switch
+    batch_->drain();                    // keep this encoder's packet order across the switch
     batch_->detach(this);
   }
   batch_ = b;
@@ -1643,7 +1722,7 @@ void Decoder::set_batch(Batch* b)
 {
   if (b == batch_) return;
   if (batch_) {
-    batch_->flush();
+    batch_->drain();
     batch_->detach(this);
   }
   if (!b) {
@@ -1700,15 +1779,39 @@ Batch::~Batch()
 
 void Batch::flush()
 {
+  // an asynchronous flush in flight: its results, then its events (they precede the queued ones)
+  if (!flight_q_.empty()) {
+    Device::get().complete();
+    std::vector<Pending> f;
+    f.swap(flight_q_);
+    emit(f);
+  }
   // every payload the queued events emit: evaluated (with what it reads) and fetched, all fields
   // and objects of the batch together
   std::vector<Node*> roots;
   for (const Pending& p : q_)
     if (p.node && !p.node->has_value()) roots.push_back(p.node.get());
-  if (!roots.empty()) Device::get().evaluate(roots);
+  if (async && !roots.empty()) {
+    Device::get().evaluate(roots, true);
+    bool all = true;                     // only w != 8 work (synchronous): nothing in flight
+    for (Node* r : roots) all = all && r->has_value();
+    if (!all) {
+      flight_q_.swap(q_);
+      if (q_.capacity() < spare_.capacity()) q_.swap(spare_);
+      return;
+    }
+  } else if (!roots.empty()) {
+    Device::get().evaluate(roots);
+  }
   std::vector<Pending> q;
   q.swap(q_);
   if (q_.capacity() < spare_.capacity()) q_.swap(spare_);   // keep the queue's storage warm
+  emit(q);
+}
+
+// the handlers of a flushed queue, in production order
+void Batch::emit(std::vector<Pending>& q)
+{
   for (Pending& p : q) {
     --(p.kind == Pending::ENC_PACKET ? p.enc->queued_ : p.dec->queued_);   // before its callback
     if (p.kind == Pending::DEC_DATA) {
@@ -1730,7 +1833,7 @@ void Batch::flush()
   for (Pending& p : q)
     if (p.pkt.capacity() && pool_.size() < 16384) pool_.push_back(std::move(p.pkt));
   q.clear();
-  spare_.swap(q);
+  if (q.capacity() > spare_.capacity()) spare_.swap(q);
 }
 
 // c/detail/check_error.hh: exceptions -> ntc_error (message in thread-local storage).
@@ -1895,6 +1998,10 @@ void ntc_decoder_set_batch(ntc_decoder_t* dec, ntc_batch_t* b, ntc_error* error)
 void ntc_batch_set_eager(ntc_batch_t* b, int on) noexcept
 {
   if (b) b->b.eager = on != 0;
+}
+void ntc_batch_set_async(ntc_batch_t* b, int on) noexcept
+{
+  if (b) b->b.async = on != 0;
 }
 
 void ntc_batch_flush(ntc_batch_t* b, ntc_error* error) noexcept

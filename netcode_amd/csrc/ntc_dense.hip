@@ -457,7 +457,12 @@ __device__ __forceinline__ void panel_run(const PanelArgs& a, PanelSmem& sm, uin
         const int en = (s + 1 < static_cast<int>(kPanel)) ? (((s + 1) >> 2) - q) : 0;
         // the record's nine entries read by inline asm too, the next column's first, so that
         // every read is older than the next step's gathers (LDS returns in order: waiting for the
-        // record never waits for the gathers)
+        // record never waits for the gathers).  The lgkmcnt values below are hand-counted: they
+        // hold only while the compiler issues no other LGKM operation in this window and does not
+        // copy an asm output register before its wait ("+v" on the wait is the only tie).
+        // Verified on ROCm 7.2 (AMD clang 22.0.0git, roc-7.2.0 26014) by disassembly; a compiler
+        // that breaks either assumption produces wrong pivot records, which the dense parity
+        // suite (tests/test_gpu_dense.py, inverses against the oracle) reports.
         u32x4 c[9];
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(c[en]) : "v"(rec0), "i"((s * 9 + en) * 16));
 #pragma unroll

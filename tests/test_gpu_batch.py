@@ -224,3 +224,51 @@ def test_eager_batch_emits_early_and_reenters(capi):
     assert ea.packets == eb.packets
     assert da.data == db.data and da.packets == db.packets
     assert db.nb_decoded > 0
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_async_batch_matches_unbatched(capi, oracle, eager):
+    """Asynchronous flushes (ntc_batch_set_async): a flush first delivers the events of the previous
+    one, then starts the device work of the queued events and returns; the objects keep producing
+    events meanwhile (queued behind the ones in flight).  Encoders and decoders on one batch,
+    across field sizes, with the decoders fed from their encoders' packets: every object's packet
+    and delivery sequence equals its unbatched twin's once the batch is drained."""
+    batch = capi.Batch(eager=eager, asynchronous=True)
+    rng = np.random.default_rng(21 + eager)
+    flows = []
+    for w, rate in ((8, 3), (16, 4), (8, 5), (4, 2)):
+        ea, eb = capi.Encoder(w), capi.Encoder(w)
+        da, db = capi.Decoder(w, in_order=True), capi.Decoder(w, in_order=True)
+        for e in (ea, eb):
+            e.set_rate(rate)
+            e.set_window_size(24)
+        for d in (da, db):
+            d.set_ack_period_ms(0)
+            d.set_ack_nb_packets(9)
+        ea.set_batch(batch)
+        da.set_batch(batch)
+        flows.append([w, ea, eb, da, db, 0, 0])
+    in_flight = 0
+    for step in range(160):
+        for f in flows:
+            w, ea, eb, da, db = f[:5]
+            n = int(rng.integers(1, 300)) * (4 if w >= 16 else 1)
+            data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            ea.add_data(data)
+            eb.add_data(data)
+            # the decoders see what their encoder has emitted so far (b's are all out already)
+            for p in ea.packets[f[5]:]:
+                if rng.random() >= 0.15:
+                    da.add_packet(p)
+                    db.add_packet(eb.packets[f[5]])
+                f[5] += 1
+        if step % 3 == 2:
+            batch.flush()
+            in_flight += batch.pending > 0
+    while batch.pending:
+        batch.flush()
+    assert in_flight > 10                 # flushes did return with work still in flight
+    for w, ea, eb, da, db, _, _ in flows:
+        assert ea.packets == eb.packets, w
+        assert da.data == db.data and da.packets == db.packets, w
+    assert sum(f[4].nb_decoded for f in flows) > 0     # repairs did decode lost sources

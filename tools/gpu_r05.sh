@@ -2,7 +2,8 @@
 # Round-5 GPU steps, one parametrised script (replaces the one-off gpu_r04*.sh launchers).
 # usage: bash tools/gpu_r05.sh <tag> <step>[,<step>...] [bench args...]
 #   steps: tests (pytest -m gpu), dense (test_gpu_dense.py only), mb (tools/mb_issue),
-#          bench (default bench line), c2|c4|c5 (per-config lines), smoke
+#          bench (default bench line), c2|c4|c5 (per-config lines), smoke, batch (adaptor
+#          tests), pp (per-packet line)
 set -o pipefail
 TAG=$1; STEPS=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p $OUT
@@ -23,6 +24,20 @@ for s in "${S[@]}"; do
     ab) run ab_lib 900 bash tools/ab_lib.sh "$AB_OTHER" "$@" ;;
     abenv) run ab_env 900 bash tools/ab_env.sh "$AB_A" "$AB_B" "$@" ;;
     abl) eval "run abl 900 bash tools/abl_run.sh $ABL -- $*" ;;
+    batch) run batch 300 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_capi.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    pp) run per_packet 400 python bench.py --per-packet "$@" ;;
+    c4pmc)  # config-4 read traffic by row pitch: FETCH_SIZE and the raw TCC read-request counters
+      for ST in ${C4_STRIDES:-1504 1536}; do
+        B="$PWD/bench.py --config k128r32s1500 --stride $ST --steps 2 --warmup 1 --no-cpu-baseline --no-host-rate"
+        run c4_line_$ST 300 python bench.py --config k128r32s1500 --stride $ST --no-cpu-baseline --no-host-rate
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OLDPWD/$OUT/c4pmc_$ST/fetch -o run -- python3 $B > $OLDPWD/$OUT/c4pmc_$ST.fetch.log 2>&1) || { echo "fetch pass $ST failed"; exit 1; }
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OLDPWD/$OUT/c4pmc_$ST/write -o run -- python3 $B > $OLDPWD/$OUT/c4pmc_$ST.write.log 2>&1) || { echo "write pass $ST failed"; exit 1; }
+        echo "c4pmc $ST done"
+      done
+      for ST in ${C4_STRIDES:-1504 1536}; do
+        B="$PWD/bench.py --config k128r32s1500 --stride $ST --steps 2 --warmup 1 --no-cpu-baseline --no-host-rate"
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -f csv -d $OLDPWD/$OUT/c4pmc_$ST/req -o run -- python3 $B > $OLDPWD/$OUT/c4pmc_$ST.req.log 2>&1) || { echo "req pass $ST failed (counter names?)"; tail -3 $OUT/c4pmc_$ST.req.log; break; }
+      done ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_shapes.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -9,7 +9,7 @@
  * encoder / decoder attached to one ntc_batch_t, flushed once per round (decoders every 4 rounds
  * and at the end).  Prints one JSON object.
  *
- * usage: pp_driver <immediate|batched> F M S W R L seed
+ * usage: pp_driver <immediate|batched|async> F M S W R L seed
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -107,10 +107,12 @@ static int check(const ntc_error* e, const char* what)
 int main(int argc, char** argv)
 {
   if (argc != 9) {
-    fprintf(stderr, "usage: %s <immediate|batched> F M S W R L seed\n", argv[0]);
+    fprintf(stderr, "usage: %s <immediate|batched|async> F M S W R L seed\n", argv[0]);
     return 2;
   }
-  const int batched = strcmp(argv[1], "batched") == 0;
+  /* "async": batched, with asynchronous flushes (each flush's GPU work overlaps the next round) */
+  const int async = strcmp(argv[1], "async") == 0;
+  const int batched = async || strcmp(argv[1], "batched") == 0;
   const uint32_t F = (uint32_t)atoi(argv[2]), M = (uint32_t)atoi(argv[3]), S = (uint32_t)atoi(argv[4]);
   const uint32_t W = (uint32_t)atoi(argv[5]), R = (uint32_t)atoi(argv[6]), L = (uint32_t)atoi(argv[7]);
   const uint64_t seed = strtoull(argv[8], NULL, 10);
@@ -128,6 +130,8 @@ int main(int argc, char** argv)
   ntc_batch_t* db = batched ? ntc_new_batch() : NULL;
   ntc_batch_set_eager(eb, 1);        /* source packets and received deliveries go out at once */
   ntc_batch_set_eager(db, 1);
+  ntc_batch_set_async(eb, async);
+  ntc_batch_set_async(db, async);
   for (uint32_t f = 0; f < F; ++f) {
     ntc_packet_handler h = {&tx[f], on_prepare, on_send};
     enc[f] = ntc_new_encoder(8, h);
@@ -159,6 +163,7 @@ int main(int argc, char** argv)
    * item into its window the same way */
   ntc_data_t** items = (ntc_data_t**)calloc(F, sizeof(void*));
   for (uint32_t f = 0; f < F; ++f) items[f] = ntc_new_data(0);
+  double t_flush_enc = 0, t_flush_dec = 0;   /* time inside ntc_batch_flush (GPU round trips) */
   prof_gate(1, "enc");
   double t0 = now();
   for (uint32_t i = 0; i < M; ++i) {
@@ -170,10 +175,19 @@ int main(int argc, char** argv)
       if (check(&err, "ntc_encoder_add_data")) return 1;
     }
     if (eb) {
+      const double tf = now();
       ntc_batch_flush(eb, &err);
+      t_flush_enc += now() - tf;
       if (check(&err, "ntc_batch_flush")) return 1;
     }
   }
+  if (eb)                           /* async: the last flush's events (a no-op otherwise) */
+    while (ntc_batch_pending(eb)) {
+      const double tf = now();
+      ntc_batch_flush(eb, &err);
+      t_flush_enc += now() - tf;
+      if (check(&err, "ntc_batch_flush")) return 1;
+    }
   const double t_enc = now() - t0;
   prof_gate(0, "enc");
   uint64_t npk = 0, nrep = 0, nrx = 0, ndel = 0;
@@ -212,14 +226,19 @@ int main(int argc, char** argv)
         if (check(&err, "ntc_decoder_add_packet")) return 1;
       }
     if (db && i % 4 == 3) {
+      const double tf = now();
       ntc_batch_flush(db, &err);
+      t_flush_dec += now() - tf;
       if (check(&err, "ntc_batch_flush")) return 1;
     }
   }
-  if (db) {
-    ntc_batch_flush(db, &err);
-    if (check(&err, "ntc_batch_flush")) return 1;
-  }
+  if (db)
+    do {                            /* async: until the last flush's events are delivered */
+      const double tf = now();
+      ntc_batch_flush(db, &err);
+      t_flush_dec += now() - tf;
+      if (check(&err, "ntc_batch_flush")) return 1;
+    } while (ntc_batch_pending(db));
   const double t_dec = now() - t0;
   prof_gate(0, "dec");
   uint64_t hp = 0xCBF29CE484222325ull, hd = 0xCBF29CE484222325ull;
@@ -228,10 +247,11 @@ int main(int argc, char** argv)
     hd = fnv(hd, rx[f].v, rx[f].n);
     ndel += rx[f].np;
   }
-  printf("{\"mode\": \"%s\", \"encode_s\": %.6f, \"decode_s\": %.6f, \"packets\": %llu, "
+  printf("{\"mode\": \"%s\", \"encode_s\": %.6f, \"decode_s\": %.6f, \"encode_flush_s\": %.6f, "
+         "\"decode_flush_s\": %.6f, \"packets\": %llu, "
          "\"received\": %llu, \"deliveries\": %llu, \"repairs\": %llu, "
          "\"packets_hash\": \"%016llx\", \"deliveries_hash\": \"%016llx\"}\n",
-         argv[1], t_enc, t_dec, (unsigned long long)npk, (unsigned long long)nrx,
+         argv[1], t_enc, t_dec, t_flush_enc, t_flush_dec, (unsigned long long)npk, (unsigned long long)nrx,
          (unsigned long long)ndel, (unsigned long long)nrep, (unsigned long long)hp,
          (unsigned long long)hd);
   for (uint32_t f = 0; f < F; ++f) {

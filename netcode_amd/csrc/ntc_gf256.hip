@@ -1933,10 +1933,21 @@ __device__ __forceinline__ void set_byte_dyn_u(uint32_t (&v)[W], uint32_t i, uin
 // dwords 0-3 of c's table at a 16-byte pitch (ds_read_b128, 16 lanes per bank cycle: bank group c
 // mod 16), dword 4 at a 4-byte pitch (ds_read_b32, 32 lanes: bank c mod 32).  With the 8-dword
 // PermTables rows every b128 gather landed on c mod 8 and every fifth-dword gather on c mod 4.
+// Rows 256 .. 259 repeat rows 1 .. 4: the table index of a coefficient straight from its folded
+// residue (coef_tidx) reaches them for residues 255 .. 258.
 struct PlanTab {
-  uint4 a[256];
-  uint32_t b[256];
+  uint4 a[260];
+  uint32_t b[260];
 };
+
+// Table row of the coefficient ((R1 + S1) * R1 mod 2^32) mod 255 + 1 (galois_field.hh:143-158)
+// without the divide: 256 = 1 (mod 255), so the byte sum of x is x mod 255 plus a multiple of 255;
+// a second byte sum folds it to 0 .. 258, and rows 256 .. 259 of PlanTab repeat rows 1 .. 4.
+__device__ __forceinline__ uint32_t coef_tidx(uint32_t R1, uint32_t S1)
+{
+  const uint32_t x = (R1 + S1) * R1;
+  return __builtin_amdgcn_sad_u8(__builtin_amdgcn_sad_u8(x, 0u, 0u), 0u, 0u) + 1u;
+}
 
 // Gauss-Jordan step for column P (compile-time, so every register index is static): false when
 // column P has no nonzero at or below row P (M singular).
@@ -2026,15 +2037,44 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   __shared__ uint16_t s_recv[kPlanWaves][RM];
   // scratch of the rank screening: received rows x (W + 1) dwords
   __shared__ __attribute__((aligned(16))) uint32_t s_scr[kPlanWaves][RM * (W + 1)];
-  for (uint32_t c = threadIdx.x; c < 256u; c += 64u * kPlanWaves) {
-    ptab.a[c] = *reinterpret_cast<const uint4*>(&d_perm.w[c][0]);
-    ptab.b[c] = d_perm.w[c][4];
-  }
-  __syncthreads();   // the only block-wide barrier: the waves below are independent generations
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = uniform(threadIdx.x >> 6);
-  const uint32_t g = blockIdx.x * kPlanWaves + wv;
-  if (g >= a.G) return;
+  const uint32_t g0 = blockIdx.x * kPlanWaves + wv;
+  const bool live = g0 < a.G;
+  const uint32_t g = live ? g0 : 0u;      // a wave past G loads generation 0's words, then leaves
+  const uint32_t k = a.k, r = a.r;
+  const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
+  const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
+  // the first two 64-source chunks' masks and lengths, this generation's repair mask and sizes:
+  // independent loads issued together, and together with the table fill below (one memory round
+  // trip before the barrier instead of one per use; k <= 128 covers every generation of
+  // configs 1-4)
+  // (unconditional loads at clamped indices, selected at first use: a load under a lane branch
+  // had its compare hoisted into the branch, which waited for the load right there)
+  uint32_t smv[2], slv[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t idx = 64u * c + lane, ci = min(idx, k - 1u);
+    const uint32_t mv = smask[ci], lv = a.src_len[static_cast<size_t>(g) * k + ci];
+    smv[c] = idx < k ? mv : 1u;
+    slv[c] = idx < k ? lv : 0u;
+  }
+  // (r = 0: element 0 of the source arrays, a valid address, never used)
+  const uint32_t ri = min(lane, max(r, 1u) - 1u);
+  const uint8_t* rm = r ? rmask : smask;
+  const uint16_t* rs = r ? a.rep_size + static_cast<size_t>(g) * r : a.src_len;
+  const uint32_t rmv_l = rm[ri], rsv_l = rs[ri];
+  const uint32_t rmv = lane < r ? rmv_l : 0u;
+  const uint32_t rsv = lane < r ? rsv_l : 0u;
+  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
+  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
+  for (uint32_t c = threadIdx.x; c < 260u; c += 64u * kPlanWaves) {
+    const uint32_t e = c < 256u ? c : c - 255u;
+    ptab.a[c] = *reinterpret_cast<const uint4*>(&d_perm.w[e][0]);
+    ptab.b[c] = d_perm.w[e][4];
+  }
+  __syncthreads();   // the only block-wide barrier: the waves below are independent generations
+  if (!live) return;
   uint16_t* miss = s_miss[wv];
   uint16_t* recv = s_recv[wv];
   uint32_t* scr = s_scr[wv];
@@ -2045,28 +2085,12 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
   };
   auto tab = [&](uint32_t c, uint32_t (&t)[5]) {
     const uint4 ab = ptab.a[c];
-    t[0] = ab.x; t[1] = ab.y; t[2] = ab.z; t[3] = ab.w; t[4] = ptab.b[c];
+    uint32_t cb = c;                 // opaque: 4c by a shift, not 16c - 12c by a 64-bit mad
+    asm volatile("" : "+v"(cb));
+    t[0] = ab.x; t[1] = ab.y; t[2] = ab.z; t[3] = ab.w; t[4] = ptab.b[cb];
   };
-
-  const uint32_t k = a.k, r = a.r;
-  const uint32_t sidb = a.sid_base ? a.sid_base[g] : g * k;
-  const uint32_t ridb = a.rid_base ? a.rid_base[g] : g * r;
-  const uint8_t* smask = a.src_mask + static_cast<size_t>(g) * k;
-  const uint8_t* rmask = a.rep_mask + static_cast<size_t>(g) * r;
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 
-  // the first two 64-source chunks' masks and lengths, this generation's repair mask and sizes:
-  // independent loads issued together (one memory round trip instead of one per use; k <= 128
-  // covers every generation of configs 1-4)
-  uint32_t smv[2], slv[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const uint32_t idx = 64u * c + lane;
-    smv[c] = idx < k ? smask[idx] : 1u;
-    slv[c] = idx < k ? a.src_len[static_cast<size_t>(g) * k + idx] : 0u;
-  }
-  const uint32_t rmv = lane < r ? rmask[lane] : 0u;
-  const uint32_t rsv = lane < r ? a.rep_size[static_cast<size_t>(g) * r + lane] : 0u;
   auto mask_at = [&](uint32_t base) -> uint32_t {      // smask of source base + lane (or 1 past k)
     const uint32_t idx = base + lane;
     if (base == 0) return smv[0];
@@ -2328,22 +2352,10 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
 #pragma unroll
         for (int w = 0; w < W; ++w) acc0[w] = acc1[w] = 0;
         const uint32_t mq = m;
-        // the coefficient tables of q+1 are looked up while q's products are formed (their LDS
-        // gathers are issued after q's selector reads, so their wait leaves them in flight)
-        uint32_t tn0[5] = {0, 0, 0, 0, 0}, tn1[5] = {0, 0, 0, 0, 0};
-        if (mq) {
-          const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, 0);
-          tab(((R1 + Sa) * R1) % 255u + 1u, tn0);
-          if (two) tab(((R1 + Sb) * R1) % 255u + 1u, tn1);
-        }
-        for (uint32_t q = 0; q < mq; ++q) {
-          uint32_t tc0[5], tc1[5];
-#pragma unroll
-          for (int e = 0; e < 5; ++e) { tc0[e] = tn0[e]; tc1[e] = tn1[e]; }
-          // column q's selector words, uniform: M^-1 column q is lane RM + q's col[] (read across
-          // lanes), its v_perm selectors formed on the scalar unit.  Broadcast LDS reads of them
-          // (6 x 16 B per lane and q) saturated the CU's LDS with 16 waves in this loop.
-          uint32_t sq[3][W];
+        // Column q's selector words, uniform: M^-1 column q is lane RM + q's col[] (read across
+        // lanes), its v_perm selectors formed on the scalar unit.  Broadcast LDS reads of them
+        // (6 x 16 B per lane and q) saturated the CU's LDS with 16 waves in this loop.
+        auto selectors = [&](uint32_t q, uint32_t (&sq)[3][W]) {
 #pragma unroll
           for (int w = 0; w < W; ++w) {
             const uint32_t cw = __builtin_amdgcn_readlane(col[w], RM + q);
@@ -2351,23 +2363,65 @@ __global__ __launch_bounds__(64 * kPlanWaves) void decode_plan_w(PlanArgs a)
             sq[1][w] = (cw >> 3) & 0x07070707u;
             sq[2][w] = (cw >> 6) & 0x03030303u;
           }
-          if (q + 1 < mq) {
-            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q + 1);
-            tab(((R1 + Sa) * R1) % 255u + 1u, tn0);
-            if (two) tab(((R1 + Sb) * R1) % 255u + 1u, tn1);
-          }
+        };
+        // Products of an even q and the next odd one share their XORs: the even step folds two of
+        // its three lookups into acc and leaves the third pending, the odd step folds that one and
+        // its own three (three bitop3 per word for two q instead of four).
+        auto mac_even = [&](const uint32_t (&t)[5], const uint32_t (&sq)[3][W], uint32_t (&acc)[W],
+                            uint32_t (&pend)[W]) {
 #pragma unroll
-          for (int w = 0; w < W; ++w)
-            acc0[w] ^= xor3(__builtin_amdgcn_perm(tc0[1], tc0[0], sq[0][w]),
-                            __builtin_amdgcn_perm(tc0[3], tc0[2], sq[1][w]),
-                            __builtin_amdgcn_perm(tc0[4], tc0[4], sq[2][w]));
-          if (two) {
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-              acc1[w] ^= xor3(__builtin_amdgcn_perm(tc1[1], tc1[0], sq[0][w]),
-                              __builtin_amdgcn_perm(tc1[3], tc1[2], sq[1][w]),
-                              __builtin_amdgcn_perm(tc1[4], tc1[4], sq[2][w]));
+          for (int w = 0; w < W; ++w) {
+            acc[w] = xor3(acc[w], __builtin_amdgcn_perm(t[1], t[0], sq[0][w]),
+                          __builtin_amdgcn_perm(t[3], t[2], sq[1][w]));
+            pend[w] = __builtin_amdgcn_perm(t[4], t[4], sq[2][w]);
           }
+        };
+        auto mac_odd = [&](const uint32_t (&t)[5], const uint32_t (&sq)[3][W], uint32_t (&acc)[W],
+                           const uint32_t (&pend)[W]) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const uint32_t a = xor3(acc[w], pend[w], __builtin_amdgcn_perm(t[1], t[0], sq[0][w]));
+            acc[w] = xor3(a, __builtin_amdgcn_perm(t[3], t[2], sq[1][w]),
+                          __builtin_amdgcn_perm(t[4], t[4], sq[2][w]));
+          }
+        };
+        // the coefficient tables of q + 1 are looked up while q's products are formed (their LDS
+        // gathers are issued after q's selector reads, so their wait leaves them in flight); two
+        // table sets alternate, so nothing is copied between iterations.  One loop per chunk
+        // count (wave-uniform), so the second chunk's registers are not carried through phis.
+        auto q_loop = [&](auto two_c) {
+          constexpr bool kT = decltype(two_c)::value;
+          auto tables = [&](uint32_t q, uint32_t (&t0)[5], uint32_t (&t1)[5]) {
+            const uint32_t R1 = __builtin_amdgcn_readlane(row_r1, q);
+            tab(coef_tidx(R1, Sa), t0);
+            if constexpr (kT) tab(coef_tidx(R1, Sb), t1);
+          };
+          uint32_t tA0[5], tA1[5], tB0[5], tB1[5];
+          uint32_t pend0[W], pend1[W];
+          tables(0, tA0, tA1);
+          for (uint32_t q = 0; q < mq; q += 2) {
+            uint32_t sq[3][W];
+            selectors(q, sq);
+            if (q + 1 < mq) tables(q + 1, tB0, tB1);
+            mac_even(tA0, sq, acc0, pend0);
+            if constexpr (kT) mac_even(tA1, sq, acc1, pend1);
+            if (q + 1 >= mq) {                     // odd m: the last pending lookups
+#pragma unroll
+              for (int w = 0; w < W; ++w) {
+                acc0[w] ^= pend0[w];
+                if constexpr (kT) acc1[w] ^= pend1[w];
+              }
+              break;
+            }
+            selectors(q + 1, sq);
+            if (q + 2 < mq) tables(q + 2, tA0, tA1);
+            mac_odd(tB0, sq, acc0, pend0);
+            if constexpr (kT) mac_odd(tB1, sq, acc1, pend1);
+          }
+        };
+        if (mq) {
+          if (two) q_loop(std::true_type{});
+          else q_loop(std::false_type{});
         }
         if (got0) {
           emit(pos0, acc0);

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -65,6 +66,32 @@ using bytes = std::vector<uint8_t, Align16<uint8_t>>;
 // payload is uploaded once, at the first flush that needs it, into a chunk of the device arena,
 // and the results that later combinations read (decoded sources, reduced repairs) stay there too.
 // A chunk is reused once no live payload points into it.
+// NTC_BATCH_PROFILE=1: where a batch flush spends its host time (seconds, summed over flushes),
+// printed to stderr at exit.  Diagnostics only; off by default (one getenv at load).
+struct BatchProf {
+  const bool on = std::getenv("NTC_BATCH_PROFILE") != nullptr;
+  double complete = 0, emit_prev = 0, roots = 0, walk = 0, stage = 0, enqueue = 0, wait = 0, emit = 0;
+  uint64_t flushes = 0, jobs = 0, terms = 0, up_bytes = 0, down_bytes = 0;
+  static double now()
+  {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  ~BatchProf()
+  {
+    if (on && flushes)
+      std::fprintf(stderr,
+                   "{\"batch_profile\": {\"flushes\": %llu, \"jobs\": %llu, \"terms\": %llu, \"up_bytes\": %llu, "
+                   "\"down_bytes\": %llu, \"complete_s\": %.6f, \"emit_prev_s\": %.6f, \"roots_s\": %.6f, "
+                   "\"walk_s\": %.6f, \"stage_s\": %.6f, \"enqueue_s\": %.6f, \"wait_s\": %.6f, \"emit_s\": %.6f}}\n",
+                   (unsigned long long)flushes, (unsigned long long)jobs, (unsigned long long)terms,
+                   (unsigned long long)up_bytes, (unsigned long long)down_bytes, complete, emit_prev, roots,
+                   walk, stage, enqueue, wait, emit);
+  }
+};
+static BatchProf g_prof;
+#define NTC_PROF_T(var) const double var = g_prof.on ? BatchProf::now() : 0.0
+#define NTC_PROF_ADD(field, since) do { if (g_prof.on) g_prof.field += BatchProf::now() - (since); } while (0)
+
 struct DevChunk {
   uint8_t* d = nullptr;
   size_t cap = 0, used = 0;
@@ -249,13 +276,14 @@ class Device {
   // Batch flush: evaluate every derived node the roots need (each after the nodes it reads),
   // then bring the roots' values to the host.  GF(2^8): payloads on the device arena, one
   // gather_combine launch per dependency level; other fields: per level one host-staged combine.
-  // async (ntc_batch_set_async): enqueue the GF(2^8) work and return; its results land in the
-  // nodes at the next complete() / evaluate() (other fields' work, host-staged, completes here).
-  // Any earlier asynchronous flush is completed first, so at most one is in flight.
-  void evaluate(const std::vector<Node*>& roots, bool async = false)
+  // async (ntc_batch_set_async): enqueue the GF(2^8) work and return its flight id (0: nothing
+  // left in flight); its results land in the nodes at complete_through(id) (other fields' work,
+  // host-staged, completes here).  Two staging sets: a flush may be launched while the previous
+  // one is still in flight; a third waits for the oldest.
+  uint64_t evaluate(const std::vector<Node*>& roots, bool async = false)
   {
     std::lock_guard<std::mutex> lock(mu_);
-    complete_locked();
+    NTC_PROF_T(t_walk);
     const uint64_t ep = ++epoch_;
     std::vector<Node*> todo;                       // dependencies first
     std::vector<std::pair<Node*, size_t>> stack;
@@ -285,16 +313,34 @@ class Device {
     std::stable_sort(todo.begin(), todo.end(), [](const Node* a, const Node* b) { return a->level < b->level; });
     std::vector<Node*> t8, tw;
     for (Node* n : todo) (n->w == 8 ? t8 : tw).push_back(n);
+    NTC_PROF_ADD(walk, t_walk);
     if (!tw.empty()) evaluate_host(tw);
-    if (!t8.empty() || !roots.empty()) evaluate_w8(t8, roots, ep, async);
+    if (t8.empty() && roots.empty()) return 0;
+    return evaluate_w8(t8, roots, ep, async);
   }
 
-  // the results of an asynchronous evaluate(): wait for its work, then values into the nodes
-  void complete()
+  // flights up to id complete: their work done, their roots' values in the nodes
+  void complete_through(uint64_t id)
   {
     std::lock_guard<std::mutex> lock(mu_);
-    complete_locked();
+    while (!flights_.empty() && flights_.front().id <= id) complete_oldest_locked();
   }
+
+  // true when flight id's work is done (never waits)
+  bool ready(uint64_t id)
+  {
+    std::lock_guard<std::mutex> lock(mu_);
+    for (const Flight& f : flights_)
+      if (f.id == id) {
+#ifndef NTC_CAPI_HOST_STUB
+        return hipEventQuery(st_[f.set].ev) == hipSuccess;
+#else
+        return true;
+#endif
+      }
+    return true;                         // completed already
+  }
+
 
  private:
   // w != 8: level by level, inputs from the host (the old per-field path)
@@ -358,9 +404,10 @@ class Device {
   // job / term descriptors go up in ONE copy into the flush's arena region; a root's result is
   // written by its job both into the arena and straight into pinned host memory (the job's second
   // output), so a flush is one copy, one launch per dependency level and one synchronisation.
-  void evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep,
-                   bool async = false)
+  uint64_t evaluate_w8(const std::vector<Node*>& todo, const std::vector<Node*>& roots, uint64_t ep,
+                       bool async)
   {
+    NTC_PROF_T(t_stage);
     const uint64_t up_mark = ep + (1ull << 63);
     std::vector<Node*> up;
     size_t up_bytes = 0, out_bytes = 0, nterms = 0;
@@ -388,24 +435,33 @@ class Device {
         late_bytes += pad16(r->size);
       }
     }
-    if (todo.empty() && late.empty()) return;
+    if (todo.empty() && late.empty()) return 0;
+    // a staging set with no flight in it (else wait for the oldest flight)
+    int si = !st_[0].busy ? 0 : !st_[1].busy ? 1 : -1;
+    if (si < 0) {
+      si = flights_.front().set;
+      complete_oldest_locked();
+    }
+    Stage& S = st_[si];
     // flush region of the arena: [uploaded payloads | descriptors | job outputs]
     const size_t desc = pad16(todo.size() * sizeof(ntc_gf256_gather_job) + nterms * sizeof(ntc_gf256_gather_term));
     const size_t region = up_bytes + (todo.empty() ? 0 : desc) + out_bytes;
     size_t base = 0;
     DevChunk* ch = region ? arena_alloc(region, &base) : nullptr;
-    grow_stage(up_bytes + desc, root_bytes + late_bytes);
+    grow_stage(S, up_bytes + desc, root_bytes + late_bytes);
+    uint8_t* const h_up = S.up;
+    uint8_t* const h_down = S.down;
     size_t pos = 0;
     for (Node* c : up) {
-      std::memcpy(h_up_ + pos, c->data(), c->size);
-      std::memset(h_up_ + pos + c->size, 0, pad16(c->size) - c->size);
+      std::memcpy(h_up + pos, c->data(), c->size);
+      std::memset(h_up + pos + c->size, 0, pad16(c->size) - c->size);
       c->chunk = ch;
       c->off = static_cast<uint32_t>(base + pos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
       pos += pad16(c->size);
     }
-    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_up_ + up_bytes);
-    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_up_ + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
+    auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_up + up_bytes);
+    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_up + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
     size_t ti = 0, opos = base + up_bytes + desc;
     for (size_t j = 0; j < todo.size(); ++j) {
       Node* n = todo[j];
@@ -413,7 +469,7 @@ class Device {
       n->off = static_cast<uint32_t>(opos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
       opos += pad16(n->size);
-      const uint64_t out2 = n->rpos != kNoPos ? reinterpret_cast<uint64_t>(h_down_ + n->rpos) : 0;
+      const uint64_t out2 = n->rpos != kNoPos ? reinterpret_cast<uint64_t>(h_down + n->rpos) : 0;
       jobs[j] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + n->off), out2,
                                      static_cast<uint32_t>(ti), static_cast<uint32_t>(n->expr.size()),
                                      n->size, 0};
@@ -421,9 +477,17 @@ class Device {
         terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(t.node->chunk->d + t.node->off),
                                             std::min<uint32_t>(t.len, n->size), t.c};
     }
+    NTC_PROF_ADD(stage, t_stage);
+    if (g_prof.on) {
+      g_prof.jobs += todo.size();
+      g_prof.terms += nterms;
+      g_prof.up_bytes += up_bytes + desc;
+      g_prof.down_bytes += root_bytes + late_bytes;
+    }
 #ifndef NTC_CAPI_HOST_STUB
+    NTC_PROF_T(t_enq);
     if (!todo.empty())
-      check(hipMemcpyAsync(ch->d + base, h_up_, up_bytes + desc, hipMemcpyHostToDevice, stream_), "H2D payloads + jobs");
+      check(hipMemcpyAsync(ch->d + base, h_up, up_bytes + desc, hipMemcpyHostToDevice, stream_), "H2D payloads + jobs");
     const auto* djobs = reinterpret_cast<const ntc_gf256_gather_job*>(todo.empty() ? nullptr : ch->d + base + up_bytes);
     const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(
         todo.empty() ? nullptr : ch->d + base + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
@@ -438,27 +502,13 @@ class Device {
     size_t lp = root_bytes;
     for (Node* r : late) {
       r->rpos = static_cast<uint32_t>(lp);
-      check(hipMemcpyAsync(h_down_ + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
+      check(hipMemcpyAsync(h_down + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
       lp += pad16(r->size);
     }
-    if (async) {
-      // in flight: the nodes count as resident for later launches (stream order), their host
-      // values and the staging are taken over by complete_locked(); the flight record keeps
-      // every node alive (an expression's terms hold its inputs' arena chunks) until then
-      check(hipEventRecord(done_, stream_), "hipEventRecord");
-      ++launches_;
-      flight_.on = true;
-      for (Node* n : todo) {
-        n->done = true;
-        flight_.todo.push_back(n->shared_from_this());
-      }
-      for (Node* r : roots)
-        if (r->derived && !r->fetched && r->rpos != kNoPos) flight_.roots.push_back(r->shared_from_this());
-      return;
-    }
-    wait_stream();
+    check(hipEventRecord(S.ev, stream_), "hipEventRecord");
+    NTC_PROF_ADD(enqueue, t_enq);
 #else
-    std::memset(h_down_, 0, root_bytes + late_bytes);
+    std::memset(h_down, 0, root_bytes + late_bytes);
     size_t lp = root_bytes;
     for (Node* r : late) {
       r->rpos = static_cast<uint32_t>(lp);
@@ -466,53 +516,89 @@ class Device {
     }
 #endif
     ++launches_;
+    // the flight: the nodes count as resident for later launches (stream order); the record
+    // keeps every node alive (an expression's terms hold its inputs' arena chunks) and remembers
+    // where each root's value lands in the set's results
+    Flight f;
+    f.id = next_flight_++;
+    f.set = si;
+    S.busy = true;
     for (Node* n : todo) {
       n->done = true;
-      n->expr.clear();
+      f.todo.push_back(n->shared_from_this());
     }
-    for (Node* r : roots) {
-      if (!r->derived || r->fetched || r->rpos == kNoPos) continue;
-      r->host.assign(h_down_ + r->rpos, h_down_ + r->rpos + r->size);
-      r->fetched = true;
-      r->rpos = kNoPos;
-    }
+    for (Node* r : roots)
+      if (r->derived && !r->fetched && r->rpos != kNoPos) {
+        f.roots.emplace_back(r->shared_from_this(), r->rpos);
+        r->rpos = kNoPos;
+      }
+    flights_.push_back(std::move(f));
+    if (async) return flights_.back().id;
+    // synchronous: this flight and any older one
+    while (!flights_.empty()) complete_oldest_locked();
+    return 0;
   }
 
-  // the in-flight asynchronous flush (at most one): its work, then its nodes' values
-  struct Flight {
-    bool on = false;
-    std::vector<NodeRef> todo, roots;
+  // flushes launched and not yet completed, oldest first, each in its own staging set
+  struct Stage {
+    uint8_t *up = nullptr, *down = nullptr;      // pinned: uploads + descriptors / results
+    size_t cap_up = 0, cap_down = 0;
+    hipEvent_t ev = nullptr;                     // recorded after the set's last copy
+    bool busy = false;                           // a flight in it
   };
-  Flight flight_;
+  struct Flight {
+    uint64_t id = 0;
+    int set = 0;
+    std::vector<NodeRef> todo;
+    std::vector<std::pair<NodeRef, uint32_t>> roots;   // root, offset of its value in set.down
+  };
+  Stage st_[2];
+  std::deque<Flight> flights_;
+  uint64_t next_flight_ = 1;
 
-  void complete_locked()
+  void wait_event(hipEvent_t ev)
   {
-    if (!flight_.on) return;
 #ifndef NTC_CAPI_HOST_STUB
+    // poll ~50 us (a flush's usual device time), then block: a long flush does not burn a core
     hipError_t e;
     const auto t0 = std::chrono::steady_clock::now();
-    while ((e = hipEventQuery(done_)) == hipErrorNotReady)
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady)
       if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
-        e = hipEventSynchronize(done_);
+        e = hipEventSynchronize(ev);
         break;
       }
-    Flight f = std::move(flight_);
-    flight_ = Flight{};
     check(e, "hipEventQuery");
 #else
-    Flight f = std::move(flight_);
-    flight_ = Flight{};
+    (void)ev;
 #endif
-    for (const NodeRef& n : f.todo) n->expr.clear();
-    for (const NodeRef& r : f.roots) {
-      if (r->fetched || r->rpos == kNoPos) continue;
-      r->host.assign(h_down_ + r->rpos, h_down_ + r->rpos + r->size);
-      r->fetched = true;
-      r->rpos = kNoPos;
-    }
   }
 
-  void grow_stage(size_t up, size_t down)
+  // the oldest flight: wait for its work, then its roots' values into the nodes (a copy out of
+  // pinned memory: reading the pinned results in place at every use measured slower)
+  void complete_oldest_locked()
+  {
+    NTC_PROF_T(t_c);
+    Flight f = std::move(flights_.front());
+    flights_.pop_front();
+    Stage& S = st_[f.set];
+    {
+      NTC_PROF_T(t_wait);
+      wait_event(S.ev);
+      NTC_PROF_ADD(wait, t_wait);
+    }
+    for (const NodeRef& n : f.todo) n->expr.clear();
+    for (auto& rp : f.roots) {
+      Node* r = rp.first.get();
+      if (r->fetched) continue;
+      r->host.assign(S.down + rp.second, S.down + rp.second + r->size);
+      r->hoff = 0;
+      r->fetched = true;
+    }
+    S.busy = false;
+    NTC_PROF_ADD(complete, t_c);
+  }
+
+  void grow_stage(Stage& S, size_t up, size_t down)
   {
     auto up_h = [](uint8_t** h, size_t* cap, size_t need) {
       if (need <= *cap) return;
@@ -527,8 +613,8 @@ class Device {
 #endif
       *cap = n;
     };
-    up_h(&h_up_, &cap_up_, up + 16);
-    up_h(&h_down_, &cap_down_, down + 16);
+    up_h(&S.up, &S.cap_up, up + 16);
+    up_h(&S.down, &S.cap_down, down + 16);
   }
 
   // combine_generations without taking mu_ (the caller holds it)
@@ -554,7 +640,8 @@ class Device {
       eng_ = nullptr;
       return;
     }
-    if (hipEventCreateWithFlags(&done_, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&st_[0].ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&st_[1].ev, hipEventDisableTiming) != hipSuccess) {
       err_ = "hipEventCreate failed";
       ntc_gf256_engine_destroy(eng_);
       eng_ = nullptr;
@@ -569,31 +656,15 @@ class Device {
     }
   }
 
-  // Wait for the flush's work by polling an event: a flush is tens of microseconds of device
-  // work with the host idle meanwhile, and a blocking synchronisation's wake-up costs a large
-  // fraction of that.
-  // Spin on the event for at most ~50 us (a flush's usual length), then block in
-  // hipEventSynchronize: a long flush does not burn a core while other threads wait on mu_.
-  void wait_stream()
-  {
-    check(hipEventRecord(done_, stream_), "hipEventRecord");
-    hipError_t e;
-    const auto t0 = std::chrono::steady_clock::now();
-    while ((e = hipEventQuery(done_)) == hipErrorNotReady) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) {
-        check(hipEventSynchronize(done_), "hipEventSynchronize");
-        return;
-      }
-    }
-    check(e, "hipEventQuery");
-  }
-
   // Once per process, when the first encoder / decoder is made: pinned staging and a first
   // arena chunk, and one flush-shaped round trip (copy engine, gather kernel) so that no
   // first-use initialisation (tens of ms on a fresh process) lands in a packet's call.
   void warm_up()
   {
-    grow_stage(size_t(4) << 20, size_t(4) << 20);
+    grow_stage(st_[1], size_t(4) << 20, size_t(4) << 20);
+    grow_stage(st_[0], size_t(4) << 20, size_t(4) << 20);
+    uint8_t* const h_up_ = st_[0].up;
+    uint8_t* const h_down_ = st_[0].down;
     size_t off = 0;
     DevChunk* ch = arena_alloc(96, &off);        // [source 16 | job 32 | term 16 | output 16]
     auto* job = reinterpret_cast<ntc_gf256_gather_job*>(h_up_ + 16);
@@ -660,9 +731,6 @@ class Device {
   std::vector<DevChunk*> chunks_;
   DevChunk* cur_ = nullptr;
   uint64_t epoch_ = 0;
-  uint8_t *h_up_ = nullptr, *h_down_ = nullptr;   // pinned: flush uploads / results
-  hipEvent_t done_ = nullptr;                       // flush completion (wait_stream)
-  size_t cap_up_ = 0, cap_down_ = 0;
 };
 
 template <typename Fill, typename Sink>
@@ -1625,8 +1693,8 @@ class Batch {
     encs_.erase(std::remove(encs_.begin(), encs_.end(), e), encs_.end());
     q_.erase(std::remove_if(q_.begin(), q_.end(), [e](const Pending& p) { return p.enc == e; }),
              q_.end());
-    flight_q_.erase(std::remove_if(flight_q_.begin(), flight_q_.end(),
-                                   [e](const Pending& p) { return p.enc == e; }), flight_q_.end());
+    for (InFlight& f : flights_)
+      f.q.erase(std::remove_if(f.q.begin(), f.q.end(), [e](const Pending& p) { return p.enc == e; }), f.q.end());
   }
   void detach(Decoder* d)
   {
@@ -1634,8 +1702,8 @@ class Batch {
     decs_.erase(std::remove(decs_.begin(), decs_.end(), d), decs_.end());
     q_.erase(std::remove_if(q_.begin(), q_.end(), [d](const Pending& p) { return p.dec == d; }),
              q_.end());
-    flight_q_.erase(std::remove_if(flight_q_.begin(), flight_q_.end(),
-                                   [d](const Pending& p) { return p.dec == d; }), flight_q_.end());
+    for (InFlight& f : flights_)
+      f.q.erase(std::remove_if(f.q.begin(), f.q.end(), [d](const Pending& p) { return p.dec == d; }), f.q.end());
   }
   void push(Pending&& p) { q_.push_back(std::move(p)); }
   // a packet buffer of an already flushed event (empty, capacity kept), or a new one
@@ -1647,7 +1715,12 @@ class Batch {
     b.clear();
     return b;
   }
-  size_t pending() const { return q_.size() + flight_q_.size(); }
+  size_t pending() const
+  {
+    size_t n = q_.size();
+    for (const InFlight& f : flights_) n += f.q.size();
+    return n;
+  }
   void flush();
   void drain()                           // every queued and in-flight event delivered
   {
@@ -1656,10 +1729,11 @@ class Batch {
     flush();
     async = a;
   }
-  // Asynchronous flushes (opt-in, ntc_batch_set_async): flush() delivers the previous flush's
-  // events, then starts the GPU work of the queued ones and returns; they are delivered by the
-  // next flush (flush until pending() is 0 to drain).  The device work of one flush overlaps
-  // whatever the caller does until the next.
+  // Asynchronous flushes (opt-in, ntc_batch_set_async): flush() delivers the events of earlier
+  // flushes whose device work is done (in order, never waiting, except for a third flush while
+  // two are in flight), then starts the device work of the queued ones and returns; they are
+  // delivered by a later flush (flush until pending() is 0 to drain).  The device work of one
+  // flush overlaps whatever the caller does until it is done.
   bool async = false;
   // Eager emission (opt-in, ntc_batch_set_eager): an event that needs no GF result -- a source
   // packet, a received source's delivery, an ack -- of an object with nothing queued goes out at
@@ -1670,7 +1744,12 @@ class Batch {
   std::vector<Encoder*> encs_;
   std::vector<Decoder*> decs_;
   std::vector<Pending> q_;
-  std::vector<Pending> flight_q_;   // an asynchronous flush's events, awaiting its results
+  struct InFlight {                // an asynchronous flush's events, awaiting its device work
+    uint64_t id;                   // Device flight (0: none of its own, waits behind the others)
+    std::vector<Pending> q;
+  };
+  std::deque<InFlight> flights_;
+
   std::vector<Pending> spare_;   // the last flushed queue's storage, reused by the next one
   void emit(std::vector<Pending>& q);
   std::vector<bytes> pool_;      // flushed packets' buffers (no malloc / free per packet)
@@ -1779,34 +1858,43 @@ Batch::~Batch()
 
 void Batch::flush()
 {
-  // an asynchronous flush in flight: its results, then its events (they precede the queued ones)
-  if (!flight_q_.empty()) {
-    Device::get().complete();
-    std::vector<Pending> f;
-    f.swap(flight_q_);
-    emit(f);
+  if (g_prof.on) ++g_prof.flushes;
+  // earlier asynchronous flushes, oldest first (their events precede the queued ones): those
+  // whose device work is done -- all of them when not asynchronous
+  while (!flights_.empty()) {
+    InFlight& f = flights_.front();
+    if (async && f.id && !Device::get().ready(f.id)) break;
+    if (f.id) Device::get().complete_through(f.id);
+    NTC_PROF_T(t_ep);
+    std::vector<Pending> q = std::move(f.q);
+    flights_.pop_front();
+    emit(q);
+    NTC_PROF_ADD(emit_prev, t_ep);
   }
   // every payload the queued events emit: evaluated (with what it reads) and fetched, all fields
   // and objects of the batch together
+  NTC_PROF_T(t_r);
   std::vector<Node*> roots;
   for (const Pending& p : q_)
     if (p.node && !p.node->has_value()) roots.push_back(p.node.get());
-  if (async && !roots.empty()) {
-    Device::get().evaluate(roots, true);
-    bool all = true;                     // only w != 8 work (synchronous): nothing in flight
-    for (Node* r : roots) all = all && r->has_value();
-    if (!all) {
-      flight_q_.swap(q_);
+  NTC_PROF_ADD(roots, t_r);
+  if (async) {
+    const uint64_t id = roots.empty() ? 0 : Device::get().evaluate(roots, true);
+    if (id || !flights_.empty()) {       // in flight, or behind flights not yet delivered
+      if (!q_.empty()) flights_.push_back(InFlight{id, std::move(q_)});
+      q_ = std::vector<Pending>();
       if (q_.capacity() < spare_.capacity()) q_.swap(spare_);
       return;
     }
   } else if (!roots.empty()) {
     Device::get().evaluate(roots);
   }
+  NTC_PROF_T(t_e);
   std::vector<Pending> q;
   q.swap(q_);
   if (q_.capacity() < spare_.capacity()) q_.swap(spare_);   // keep the queue's storage warm
   emit(q);
+  NTC_PROF_ADD(emit, t_e);
 }
 
 // the handlers of a flushed queue, in production order

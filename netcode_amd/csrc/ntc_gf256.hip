@@ -2484,14 +2484,20 @@ __global__ __launch_bounds__(64) void gather_combine(const ntc_gf256_gather_job*
   const uint32_t col = blockIdx.y * 1024u + threadIdx.x * 16u;
   if (col >= ((jlen + 15u) & ~15u)) return;
   uint32_t acc[4] = {0, 0, 0, 0};
-  for (uint32_t t = 0; t < j4[3]; ++t) {
-    const u32x4 t4 = const_load<u32x4>(terms + j4[2] + t);          // src (2 dwords), len, coef
+  // one term: its piece (zero past the term's length), times its coefficient, into acc
+  auto piece = [&](const u32x4 t4) -> uint4 {
     const uint32_t tlen = t4[2];
-    if (col >= tlen) continue;
     const uint8_t* src = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(t4[1]) << 32) | t4[0]);
-    const uint4 v = *reinterpret_cast<const uint4*>(src + col);
+    return col < tlen ? *reinterpret_cast<const uint4*>(src + col) : make_uint4(0, 0, 0, 0);
+  };
+  auto table = [&](const u32x4 t4, uint32_t (&tf)[5]) {
+    const uint32_t* tb = d_perm.w[t4[3] & 0xFFu];
+    tf[0] = tb[0]; tf[1] = tb[1]; tf[2] = tb[2]; tf[3] = tb[3]; tf[4] = tb[4];
+  };
+  auto add = [&](const u32x4 t4, const uint4 v, const uint32_t (&tf)[5]) {
     uint32_t x[4] = {v.x, v.y, v.z, v.w};
-    const uint32_t rem = tlen - col;                   // bytes of this piece that take part
+    const uint32_t tlen = t4[2];
+    const uint32_t rem = tlen > col ? tlen - col : 0u;    // bytes of this piece that take part
     if (rem < 16u) {
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -2499,10 +2505,32 @@ __global__ __launch_bounds__(64) void gather_combine(const ntc_gf256_gather_job*
         x[d] &= keep >= 4u ? 0xFFFFFFFFu : (1u << (8u * keep)) - 1u;
       }
     }
-    const uint32_t* tb = d_perm.w[t4[3] & 0xFFu];
-    const uint32_t tf[5] = {tb[0], tb[1], tb[2], tb[3], tb[4]};
 #pragma unroll
     for (int d = 0; d < 4; ++d) acc[d] ^= mul4(tf, x[d]);
+  };
+  // four terms per step: their descriptors in one scalar load, then their four tables and four
+  // pieces in flight together (a job's terms are a dependent chain of descriptor -> piece and
+  // table loads otherwise)
+  const uint32_t nt = j4[3], t0 = j4[2];
+  uint32_t t = 0;
+  for (; t + 4 <= nt; t += 4) {
+    u32x4 d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = const_load<u32x4>(terms + t0 + t + i);
+    uint32_t tf[4][5];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) table(d[i], tf[i]);
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = piece(d[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) add(d[i], v[i], tf[i]);
+  }
+  for (; t < nt; ++t) {
+    const u32x4 d = const_load<u32x4>(terms + t0 + t);
+    uint32_t tf[5];
+    table(d, tf);
+    add(d, piece(d), tf);
   }
   *reinterpret_cast<uint4*>(out + col) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
   if (out2) *reinterpret_cast<uint4*>(out2 + col) = make_uint4(acc[0], acc[1], acc[2], acc[3]);

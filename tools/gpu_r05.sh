@@ -25,6 +25,10 @@ for s in "${S[@]}"; do
     abenv) run ab_env 900 bash tools/ab_env.sh "$AB_A" "$AB_B" "$@" ;;
     abl) eval "run abl 900 bash tools/abl_run.sh $ABL -- $*" ;;
     batch) run batch 300 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_capi.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    ppprof) for M in batched async; do   # per-packet C driver with the flush profile (NTC_BATCH_PROFILE)
+        NTC_BATCH_PROFILE=1 run pp_prof_$M 120 tests/_build/pp_driver $M 256 128 1024 32 4 10 7; done ;;
+    ppsamp) for M in batched async; do for P in enc dec; do  # host sampling profile (exp/prof build)
+        NTC_SAMPLER_GATED=1 PP_PROFILE=$P NTC_SAMPLER_OUT=$OUT/samples_${M}_$P.txt run pp_samp_${M}_$P 120 exp/prof/pp_driver_prof $M 256 128 1024 32 4 10 7; done; done ;;
     pp) run per_packet 400 python bench.py --per-packet "$@" ;;
     c4pmc)  # config-4 read traffic by row pitch: FETCH_SIZE and the raw TCC read-request counters
       for ST in ${C4_STRIDES:-1504 1536}; do

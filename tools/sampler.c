@@ -23,7 +23,15 @@ static volatile long g_n = 0;
 /* NTC_SAMPLER_GATED=1: record only between ntc_sampler_enable(1) and ntc_sampler_enable(0), which
  * a program under study looks up with dlsym(RTLD_DEFAULT, ...) around its timed region */
 static volatile int g_on = 1;
-void ntc_sampler_enable(int on) { g_on = on; }
+static void start_timer(void);
+static int g_started = 0;
+/* gated: the timer itself starts at the first enable, so no signal lands in the program's start-up
+ * (a GPU runtime's initialisation does not tolerate interrupted system calls everywhere) */
+void ntc_sampler_enable(int on)
+{
+  if (on && !g_started) start_timer();
+  g_on = on;
+}
 static uintptr_t g_stk_lo = 0, g_stk_hi = 0;
 static timer_t g_timer;
 static int g_have_timer = 0;   /* main thread stack: frames are walked only inside */
@@ -66,6 +74,12 @@ __attribute__((constructor)) static void start(void)
   sa.sa_sigaction = on_prof;
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigaction(SIGPROF, &sa, NULL);
+  if (g_on) start_timer();
+}
+
+static void start_timer(void)
+{
+  g_started = 1;
   /* a wall-clock POSIX timer (hrtimer): CPU-time timers tick at the kernel HZ here (a few ms);
    * profile a single busy thread */
   struct sigevent sev;

@@ -56,6 +56,13 @@ struct Align16 {
     return static_cast<T*>(p);
   }
   void deallocate(T* p, size_t) { ::operator delete(p, std::align_val_t(16)); }
+  // resize(n) default-initialises (no zeroing), like the reference's byte_buffer (buffer.hh:66-73);
+  // resize(n, 0) and assign(n, 0) still zero-fill
+  template <typename U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+  template <typename U, typename... A> void construct(U* p, A&&... a)
+  {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
   template <typename U> bool operator==(const Align16<U>&) const { return true; }
   template <typename U> bool operator!=(const Align16<U>&) const { return false; }
 };
@@ -893,10 +900,17 @@ class Encoder {
   Encoder(Encoder&&) = default;
   ~Encoder();
 
-  // encoder.hh:255-285
-  void add_data(bytes&& d)
+  // encoder.hh:255-285.  Returns the buffer of the source that left the window when nothing
+  // else holds it (empty otherwise): the caller's data object takes it, so a steady stream of
+  // items reuses the window's buffers instead of allocating one per item.
+  bytes add_data(bytes&& d)
   {
-    if (window_.size() == window_size_) window_.pop_front();
+    bytes spare;
+    if (window_.size() == window_size_) {
+      const NodeRef& old = window_.front().sym;
+      if (old.use_count() == 1 && old->hoff == 0) spare = std::move(old->host);
+      window_.pop_front();
+    }
     auto nd = std::make_shared<Node>();
     nd->size = static_cast<uint16_t>(d.size());
     nd->host = std::move(d);
@@ -923,6 +937,7 @@ class Encoder {
     }
     if ((cur_sid_ + 1) % rate_ == 0) generate_repair();
     ++cur_sid_;
+    return spare;
   }
 
   // encoder.hh:162-169, 321-333 + detail/encoder.cc:15-64 (the combination runs on the GPU; with
@@ -1421,7 +1436,7 @@ class Decoder {
     Src s{id, bytes(), sz, nullptr};
     if (batch_) s.node = own ? adopt_node(std::move(*own), sym - own->data(), sz) : base_node(sym, sz);
     else s.sym.assign(sym, sym + sz);
-    if (!batch_ && s.sym.empty()) s.sym.resize(1);
+    if (!batch_ && s.sym.empty()) s.sym.resize(1, 0);
     add_source_recursive(std::move(s));
     attempt_full_decoding();
   }
@@ -1441,7 +1456,7 @@ class Decoder {
       r.red.push_back(Term{own ? adopt_node(std::move(*own), sym - own->data(), symsz) : base_node(sym, symsz),
                            1, symsz});
     else r.sym.assign(sym, sym + symsz);
-    if (!batch_ && r.sym.empty()) r.sym.resize(1);
+    if (!batch_ && r.sym.empty()) r.sym.resize(1, 0);
     std::vector<const Src*> known;
     std::vector<uint32_t> remaining;
     for (auto it = r.ids.rbegin(); it != r.ids.rend(); ++it) {
@@ -1984,7 +1999,7 @@ char* ntc_data_buffer(ntc_data_t* d) noexcept { return reinterpret_cast<char*>(d
 uint16_t ntc_data_get_size(const ntc_data_t* d) noexcept { return static_cast<uint16_t>(d->v.size()); }
 void ntc_data_resize(ntc_data_t* d, uint16_t n, ntc_error* error) noexcept
 {
-  ntcx::guarded([&] { d->v.resize(n, 0); }, error);
+  ntcx::guarded([&] { d->v.resize(n); }, error);      // data.hh: bytes past the old size unset
 }
 
 // --------------------------------------------------------------------------- packet ----
@@ -2017,7 +2032,8 @@ void ntc_encoder_add_data(ntc_encoder_t* enc, ntc_data_t* data, ntc_error* error
   ntcx::guarded([&] {
     ntcx::bytes v = std::move(data->v);
     data->v = ntcx::bytes();                       // moved-from: empty until resized
-    enc->e.add_data(std::move(v));
+    data->v = enc->e.add_data(std::move(v));       // (with a recycled buffer's capacity)
+    data->v.clear();
   }, error);
 }
 size_t ntc_encoder_add_packet(ntc_encoder_t* enc, ntc_packet_t* packet, ntc_error* error) noexcept

@@ -891,7 +891,8 @@ struct Pending {
   bytes pkt;                           // wire bytes
   NodeRef node;                        // encoder repair / delivered data: the payload to emit
   uint16_t size = 0;                   // repair symbol size / data size
-  size_t off1 = 0, off2 = 0;           // encoder repair: the two symbol copies inside pkt
+  size_t off1 = 0, off2 = 0;           // encoder repair: where the two symbol copies go in pkt
+                                       // (not stored there: emitted from the node, handlers.h)
 };
 
 class Encoder {
@@ -974,19 +975,17 @@ class Encoder {
     ++nb_sent_packets_;
     Pending p;
     p.enc = this;
-    begin(p, 15 + 2 * size_t(symsz) + 4 + 3 * ids_.size());
+    begin(p, 15 + 4 + 3 * ids_.size());
     out_.u8(1);                                    // packetizer.hh:90-122
     out_.u32(rid);
     out_.u16(symsz);
     p.off1 = batch_ ? p.pkt.size() : 0;
-    if (batch_) p.pkt.resize(p.pkt.size() + symsz);          // filled at flush
-    else out_.raw(sym.data(), symsz);
+    if (!batch_) out_.raw(sym.data(), symsz);                // batched: emitted at flush
     out_.ids(ids_);
     out_.u16(esz);
     out_.u16(symsz);
     p.off2 = batch_ ? p.pkt.size() : 0;
-    if (batch_) p.pkt.resize(p.pkt.size() + symsz);
-    else out_.raw(sym.data(), symsz);
+    if (!batch_) out_.raw(sym.data(), symsz);
     out_.end();
     if (batch_) {
       p.size = symsz;
@@ -1924,13 +1923,22 @@ void Batch::emit(std::vector<Pending>& q)
       h.read_data(h.context, reinterpret_cast<const char*>(d), p.size);
       continue;
     }
-    if (p.node) {                        // encoder repair: both copies of the symbol
-      std::memcpy(p.pkt.data() + p.off1, p.node->data(), p.size);
-      std::memcpy(p.pkt.data() + p.off2, p.node->data(), p.size);
-    }
     const ntc_packet_handler& h = p.kind == Pending::ENC_PACKET ? p.enc->handler()
                                                                 : p.dec->packet_handler();
-    h.prepare_packet(h.context, reinterpret_cast<const char*>(p.pkt.data()), p.pkt.size());
+    const char* pk = reinterpret_cast<const char*>(p.pkt.data());
+    if (p.node) {
+      // encoder repair: the packet's pieces around the two copies of the symbol, the symbol
+      // straight from its payload (prepare_packet may be called several times per packet,
+      // handlers.h; packetizer.hh:90-122 writes a repair the same way)
+      const char* sym = reinterpret_cast<const char*>(p.node->data());
+      h.prepare_packet(h.context, pk, p.off1);
+      h.prepare_packet(h.context, sym, p.size);
+      h.prepare_packet(h.context, pk + p.off1, p.off2 - p.off1);
+      h.prepare_packet(h.context, sym, p.size);
+      if (p.pkt.size() > p.off2) h.prepare_packet(h.context, pk + p.off2, p.pkt.size() - p.off2);
+    } else {
+      h.prepare_packet(h.context, pk, p.pkt.size());
+    }
     h.send_packet(h.context);
   }
   for (Pending& p : q)

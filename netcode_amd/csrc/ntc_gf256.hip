@@ -453,6 +453,16 @@ __device__ __forceinline__ T const_load(const void* p)
       reinterpret_cast<uintptr_t>(p));
 }
 
+// A u16 of a device array through the scalar unit (the aligned dword around it): a decode MAC
+// wave's row count comes from the plan this way, beside the kernel arguments, instead of through
+// a vector load whose whole memory round trip preceded everything else the wave issued.
+__device__ __forceinline__ uint32_t const_load_u16(const uint16_t* p)
+{
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t w = const_load<uint32_t>(reinterpret_cast<const void*>(a & ~static_cast<uintptr_t>(3)));
+  return (w >> (8u * static_cast<uint32_t>(a & 2u))) & 0xFFFFu;
+}
+
 // Source staging: every wave streams its sources through a private ring of kBsRing LDS slots with
 // LDS-DMA (global_load_lds_dwordx4), kBsRing-1 sources ahead, so HBM latency hides behind ~3
 // chain iterations without holding VGPRs.  A lane owns two 16-byte pieces of the 2 KiB column
@@ -738,7 +748,7 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
   }
   const uint32_t g = task;
   if (g >= a.G) return;
-  const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
+  const uint32_t total = DEC ? const_load_u16(a.rows_per_gen + g) : a.rows;
   const uint32_t row0 = tile * R;
   if (row0 >= total) return;
   const uint32_t nrows = min(static_cast<uint32_t>(R), total - row0);
@@ -955,7 +965,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void g
   const uint32_t g = task;
   // a group with nothing to do still takes part in the block's barriers (the other group's
   // steps): it runs k steps with no rows and builds nothing -- see bs_group's `idle`
-  const uint32_t total = g < a.G ? (DEC ? uniform(a.rows_per_gen[g]) : a.rows) : 0u;
+  const uint32_t total = g < a.G ? (DEC ? const_load_u16(a.rows_per_gen + g) : a.rows) : 0u;
   const bool idle = grp * NT * 16u >= total;           // uniform over the group
   const uint32_t tile = grp * NT + w;
   const uint32_t row0 = tile * 16u;
@@ -1005,7 +1015,7 @@ __global__ __launch_bounds__(256) void gf_mac(MacArgs a)
   const uint32_t rc = task % a.nrowchunks;
   const uint32_t g = task / a.nrowchunks;
   if (g >= a.G) return;
-  const uint32_t total = DEC ? uniform(a.rows_per_gen[g]) : a.rows;
+  const uint32_t total = DEC ? const_load_u16(a.rows_per_gen + g) : a.rows;
   const uint32_t row0 = rc * 32u;
   if (row0 >= total) return;
   const uint32_t nrows = min(32u, total - row0);

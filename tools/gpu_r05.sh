@@ -24,7 +24,8 @@ for s in "${S[@]}"; do
     ab) run ab_lib 900 bash tools/ab_lib.sh "$AB_OTHER" "$@" ;;
     abenv) run ab_env 900 bash tools/ab_env.sh "$AB_A" "$AB_B" "$@" ;;
     abl) eval "run abl 900 bash tools/abl_run.sh $ABL -- $*" ;;
-    batch) run batch 300 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_capi.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    batch) run batch 300 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_capi.py tests/test_gpu_gather.py -x -q -m gpu --timeout 120 --timeout-method thread ;;
+    surface) run surface 600 python -u -m pytest tests/test_gpu_cpp_surface.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     ppprof) for M in batched async; do   # per-packet C driver with the flush profile (NTC_BATCH_PROFILE)
         NTC_BATCH_PROFILE=1 run pp_prof_$M 120 tests/_build/pp_driver $M 256 128 1024 32 4 10 7; done ;;
     ppsamp) for M in batched async; do for P in enc dec; do  # host sampling profile (exp/prof build)

@@ -272,3 +272,60 @@ def test_async_batch_matches_unbatched(capi, oracle, eager):
         assert ea.packets == eb.packets, w
         assert da.data == db.data and da.packets == db.packets, w
     assert sum(f[4].nb_decoded for f in flows) > 0     # repairs did decode lost sources
+
+
+def test_async_batch_switch_and_delete_with_work_in_flight(capi, oracle):
+    """Asynchronous flushes leave device work in flight: a decoder leaving the batch mid-stream
+    drains it first (its deliveries stay in order, then immediate), and a batch deleted with
+    events in flight discards them without disturbing a second batch's flushes."""
+    rng = np.random.default_rng(31)
+    batch = capi.Batch(asynchronous=True)
+    ea, eb = capi.Encoder(), capi.Encoder()
+    da, db = capi.Decoder(in_order=True), capi.Decoder(in_order=True)
+    for e in (ea, eb):
+        e.set_rate(3)
+        e.set_window_size(16)
+    for d in (da, db):
+        d.set_ack_period_ms(0)
+    ea.set_batch(batch)
+    da.set_batch(batch)
+    sent = 0
+    for step in range(120):
+        data = rng.integers(0, 256, int(rng.integers(1, 500)), dtype=np.uint8).tobytes()
+        ea.add_data(data)
+        eb.add_data(data)
+        batch.flush()                      # returns with this round's work in flight
+        for p in eb.packets[sent:]:
+            if rng.random() >= 0.2:
+                da.add_packet(p)
+                db.add_packet(p)
+        sent = len(eb.packets)
+        if step == 70:
+            da.set_batch(None)             # drains the batch (in flight included), then immediate
+    while batch.pending:
+        batch.flush()
+    assert ea.packets == eb.packets
+    assert da.data == db.data and da.packets == db.packets
+    assert db.nb_decoded > 0
+    # a second asynchronous batch; the first is deleted with its encoder's events in flight
+    b2 = capi.Batch(asynchronous=True)
+    ec, ed = capi.Encoder(), capi.Encoder()
+    for e in (ec, ed):
+        e.set_rate(2)
+    ec.set_batch(b2)
+    ea.set_batch(batch)
+    for step in range(40):
+        data = bytes([step]) * (50 + step)
+        ea.add_data(data)
+        ec.add_data(data)
+        ed.add_data(data)
+        batch.flush()
+        b2.flush()
+    h, batch.h = batch.h, None             # deleted with ea's events in flight: discarded
+    batch.L.ntc_delete_batch(h)
+    n0 = len(ea.packets)
+    ea.add_data(b"after")                  # ea is unbatched again: immediate
+    assert len(ea.packets) > n0
+    while b2.pending:
+        b2.flush()
+    assert ec.packets == ed.packets

@@ -37,6 +37,7 @@ struct ntc_gf256_engine {
   size_t row_ptr_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;
   uint32_t rowtile_force = 0;  // bit-sliced row tile 8 or 16 (NTC_GF256_ROWTILE; 0 = by rows)
+  uint32_t ksplit_force = 0;   // split-k part count 1..8 (NTC_GF256_KSPLIT; 0 = the heuristic)
   int plan_kind = NTC_GF256_PLAN_AUTO;
   // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
   bool timing = false;

@@ -2727,6 +2727,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       // >= 8/3 rounds: measured at n = 1024 (2048 tasks), ksplit 2 / 3 / 4 / 6 / 8 -> MAC 1.01 /
       // 0.93 / 0.90 / 0.93 / 0.90 ms, reduce 0.028 / 0.038 / 0.050 / 0.082 / 0.117 ms per call
       uint32_t ks = static_cast<uint32_t>(std::min<uint64_t>((8 * slots + 3 * tasks - 1) / (3 * tasks), 8));
+      if (e->ksplit_force) ks = e->ksplit_force;        // experiments (NTC_GF256_KSPLIT)
       ks = std::min(ks, a.k / 64);
       const uint32_t kpart = (a.k + ks - 1) / ks;
       a.kpart = (kpart + 3) / 4 * 4;
@@ -2882,6 +2883,10 @@ int ntc_gf256_engine_create(int device, ntc_gf256_engine** out)
     if (!std::strcmp(m, "perm")) e->mac_kind = NTC_GF256_MAC_PERM;
     else if (!std::strcmp(m, "bitslice")) e->mac_kind = NTC_GF256_MAC_BITSLICE;
     else if (!std::strcmp(m, "grouped")) e->mac_kind = NTC_GF256_MAC_BITSLICE_GROUPED;
+  }
+  if (const char* t = std::getenv("NTC_GF256_KSPLIT")) {
+    const int v = std::atoi(t);
+    if (v >= 1 && v <= 8) e->ksplit_force = static_cast<uint32_t>(v);
   }
   if (const char* t = std::getenv("NTC_GF256_ROWTILE")) {
     if (!std::strcmp(t, "8")) e->rowtile_force = 8;

@@ -3,7 +3,9 @@
 # usage: bash tools/gpu_r05.sh <tag> <step>[,<step>...] [bench args...]
 #   steps: tests (pytest -m gpu), dense (test_gpu_dense.py only), mb (tools/mb_issue),
 #          bench (default bench line), c2|c4|c5 (per-config lines), smoke, batch (adaptor
-#          tests), pp (per-packet line)
+#          tests), pp (per-packet line), ppprof / ppsamp (flush / sampling profiles), c4pmc,
+#          surface, gatherab / gfwab (A/B against $AB_OTHER), ksplit (config-5 sweep)
+#   round-end evidence: tools/gpu_final_r05.sh
 set -o pipefail
 TAG=$1; STEPS=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p $OUT
@@ -43,6 +45,21 @@ for s in "${S[@]}"; do
         B="$PWD/bench.py --config k128r32s1500 --stride $ST --steps 2 --warmup 1 --no-cpu-baseline --no-host-rate"
         (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -f csv -d $OLDPWD/$OUT/c4pmc_$ST/req -o run -- python3 $B > $OLDPWD/$OUT/c4pmc_$ST.req.log 2>&1) || { echo "req pass $ST failed (counter names?)"; tail -3 $OUT/c4pmc_$ST.req.log; break; }
       done ;;
+    gatherab)  # adaptor tests on the in-tree libraries, then with libntc_gf256.so = $AB_OTHER (scratch copy)
+      T="tests/test_gpu_gather.py tests/test_gpu_batch.py tests/test_gpu_capi.py"
+      run gather_cur 300 python -u -m pytest $T -q -m gpu --timeout 120 --timeout-method thread
+      cp "$AB_OTHER" netcode_amd/libntc_gf256.so
+      run gather_other 300 python -u -m pytest $T -q -m gpu --timeout 120 --timeout-method thread ;;
+    gfwab)     # GF(2^w) parity, then tools/bench_gfw.py interleaved against $AB_OTHER
+      run gfw_tests 300 python -u -m pytest tests/test_gpu_gfw.py -x -q -m gpu --timeout 120 --timeout-method thread
+      for rep in 1 2; do
+        run gfw_cur_$rep 120 python tools/bench_gfw.py
+        NTC_GF256_LIB=$AB_OTHER run gfw_other_$rep 120 python tools/bench_gfw.py
+      done ;;
+    ksplit)    # config-5 split-k part counts ($KS, default "3 4 5 6"), two interleaved reps
+      for rep in 1 2; do for k in ${KS:-3 4 5 6}; do
+        NTC_GF256_KSPLIT=$k run ks${k}_$rep 300 python bench.py --config k1024dense --no-cpu-baseline --no-host-rate
+      done; done ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_shapes.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

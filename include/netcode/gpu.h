@@ -71,7 +71,10 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
  * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice|grouped environment variable
  * overrides AUTO process-wide.  BITSLICE runs one independent wave per row tile (gf_mac_bs);
  * BITSLICE_GROUPED (experimental, slower on MI355X: DESIGN.md §3) runs pairs of 16-row tiles per
- * workgroup that build each source's bit planes once and share them through LDS (gf_mac_bsg). */
+ * workgroup that build each source's bit planes once and share them through LDS (gf_mac_bsg).
+ * Two more environment variables, for experiments only (results identical): NTC_GF256_ROWTILE=8|16
+ * fixes the bit-sliced row tile (default: 16 when a tile has more than 8 rows), NTC_GF256_KSPLIT=n
+ * (1..8) fixes the split-k part count of encodes with too few tasks to fill the GPU. */
 enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2,
        NTC_GF256_MAC_BITSLICE_GROUPED = 3 };
 int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);

@@ -533,7 +533,11 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
   static_assert(R == 8 || R == 16, "8- or 16-row tiles");
   static_assert(!PAIR || (!DEC && !FULL), "pairing is an encode mode for short symbols");
   static_assert(kBsRing == 4, "the unrolled loop assumes a 4-slot ring");
+#ifdef NTC_ABL_KLATE       // timing-only experiment builds: the late source read for every 16-row tile
+  constexpr bool kLate = R == 16;
+#else
   constexpr bool kLate = R == 16 && !FULL;
+#endif
   using CoefV = typename BsCoef<R>::T;
   const size_t stride = a.stride;
   const uint32_t k = i_count ? i_count : a.k;           // sources this wave sums (split-k: a part)
@@ -613,6 +617,17 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
       for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
 #ifndef NTC_ABL_NOFILL     // timing-only ablation builds (tools/build_variant.sh -DNTC_ABL_...)
       transpose8(Y);
+#endif
+#ifdef NTC_ABL_FILL2       // timing-only: a second transpose of the same source, results discarded
+      {
+        uint32_t salt = 0, Z[8];
+        asm volatile("" : "+v"(salt));
+#pragma unroll
+        for (int p = 0; p < 8; ++p) Z[p] = ycur[p] ^ salt;
+        transpose8(Z);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) asm volatile("" :: "v"(Z[p]));
+      }
 #endif
       if constexpr (!kLate) {
         vm_wait<2 * (kBsRing - 3)>();                  // source i+1 has landed

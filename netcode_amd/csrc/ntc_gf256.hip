@@ -624,7 +624,11 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
         asm volatile("" : "+v"(salt));
 #pragma unroll
         for (int p = 0; p < 8; ++p) Z[p] = ycur[p] ^ salt;
+#ifdef NTC_ABL_FILL2_VGPR  // the extra transpose with register masks and shift amounts
+        transpose8<true>(Z, tmasks<true>());
+#else
         transpose8(Z);
+#endif
 #pragma unroll
         for (int p = 0; p < 8; ++p) asm volatile("" :: "v"(Z[p]));
       }

@@ -759,6 +759,8 @@ def kernel_summary(log, steps, dense):
                 seen_dense += 1
             elif name == "other":                     # the split-k MAC's part reduction
                 name = "ksplit_reduce"
+            elif name == "preslice":                  # a tall MAC's source pre-slicing pass
+                name = "source_preslice"
             tot[name] = tot.get(name, 0.0) + ms
             if name in launches:
                 launches[name].append(ms)

@@ -72,9 +72,12 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
  * overrides AUTO process-wide.  BITSLICE runs one independent wave per row tile (gf_mac_bs);
  * BITSLICE_GROUPED (experimental, slower on MI355X: DESIGN.md §3) runs pairs of 16-row tiles per
  * workgroup that build each source's bit planes once and share them through LDS (gf_mac_bsg).
- * Two more environment variables, for experiments only (results identical): NTC_GF256_ROWTILE=8|16
- * fixes the bit-sliced row tile (default: 16 when a tile has more than 8 rows), NTC_GF256_KSPLIT=n
- * (1..8) fixes the split-k part count of encodes with too few tasks to fill the GPU. */
+ * An encode / combine with >= 384 rows over whole 2 KiB spans (BITSLICE or AUTO) first bit-slices
+ * its sources into an engine buffer (one HBM pass), so the MAC's row tiles skip the per-tile
+ * transpose.  More environment variables, for experiments only (results identical):
+ * NTC_GF256_ROWTILE=8|16 fixes the bit-sliced row tile (default: 16 when a tile has more than 8
+ * rows), NTC_GF256_KSPLIT=n (1..8) fixes the split-k part count of encodes with too few tasks to
+ * fill the GPU, NTC_GF256_SLICE=0|1 turns the source pre-slicing off / on for every eligible call. */
 enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2,
        NTC_GF256_MAC_BITSLICE_GROUPED = 3 };
 int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);
@@ -104,7 +107,8 @@ int  ntc_gf256_mac_time(ntc_gf256_engine* eng, int dec, float* ms);
  * microseconds that matter for sub-millisecond steps. */
 enum { NTC_GF256_K_ENCODE_PREP = 0, NTC_GF256_K_ENCODE_MAC = 1, NTC_GF256_K_DECODE_PLAN = 2,
        NTC_GF256_K_PLAN_ROWS = 3, NTC_GF256_K_DECODE_MAC = 4, NTC_GF256_K_BJ_OFFSETS = 5 /* reserved */,
-       NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 /* the split-k MAC's part reduction */ };
+       NTC_GF256_K_DENSE = 6, NTC_GF256_K_OTHER = 7 /* the split-k MAC's part reduction */,
+       NTC_GF256_K_SLICE = 8 /* a tall encode / combine's source pre-slicing pass */ };
 int  ntc_gf256_timing_log(ntc_gf256_engine* eng, uint32_t capacity);
 int  ntc_gf256_timing_kinds(ntc_gf256_engine* eng, uint32_t mask);
 int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uint32_t* kinds,
@@ -113,7 +117,9 @@ int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uin
 /* Pre-size the decode workspace for (G, k, r) so later calls never allocate (graph capture).
  * A bit-sliced encode / combine with fewer tasks than one round of wave slots (few generations,
  * k >= 128) splits its sources (split-k) and sizes its partial outputs on first use; a call
- * captured before that first use runs unsplit instead of allocating (identical results). */
+ * captured before that first use runs unsplit instead of allocating (identical results).  The
+ * pre-sliced source copy of a tall encode / combine is sized the same way (captured before its
+ * first use: the MAC slices in registers instead). */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
 
 /* Encode: rep[g][j] = sum_i c(rid_base[g]+j, sid_base[g]+i) * src[g][i] over GF(2^8)/0x11D.

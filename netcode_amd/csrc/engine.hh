@@ -29,6 +29,9 @@ struct ntc_gf256_engine {
   void* kout = nullptr;
   size_t kout_cap = 0;
   uint32_t ncu = 0;
+  // bit-sliced copy of a tall encode / combine's sources (launch_mac, bs_preslice)
+  void* slice = nullptr;
+  size_t slice_cap = 0;
   // the last plan also wrote the decode MAC's input row addresses (row_ptr) for these buffers
   const uint8_t* rows_src = nullptr;
   const uint8_t* rows_rep = nullptr;
@@ -38,6 +41,7 @@ struct ntc_gf256_engine {
   int mac_kind = NTC_GF256_MAC_AUTO;
   uint32_t rowtile_force = 0;  // bit-sliced row tile 8 or 16 (NTC_GF256_ROWTILE; 0 = by rows)
   uint32_t ksplit_force = 0;   // split-k part count 1..8 (NTC_GF256_KSPLIT; 0 = the heuristic)
+  int slice_force = -1;        // pre-sliced sources 0 / 1 (NTC_GF256_SLICE; -1 = by rows)
   int plan_kind = NTC_GF256_PLAN_AUTO;
   // MAC kernel timing (ntc_gf256_set_timing): events bracket the last encode / decode MAC launch
   bool timing = false;

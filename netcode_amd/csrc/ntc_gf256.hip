@@ -522,8 +522,9 @@ template <> struct BsCoef<16> { using T = u32x4; };
 // from one lane offset; else each piece has its own, clamped to the span's first bytes when it
 // lies past the stride (loaded, never stored).  PAIR (encode, stride <= 1024): the second piece
 // of each lane holds the same bytes of the partner generation (poff_in / poff_out bytes further
-// on; 0 and never stored when the generation is alone).
-template <int R, bool DEC, bool FULL, bool PAIR = false>
+// on; 0 and never stored when the generation is alone).  SL (encode / combine, FULL): in0 holds
+// the sources already bit-sliced by bs_preslice, so the fill is the plane tables alone.
+template <int R, bool DEC, bool FULL, bool PAIR = false, bool SL = false>
 __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t tile,
                                         uint32_t nrows, uint32_t cc, uint32_t lane, uint32_t ring,
                                         uint64_t poff_in = 0, uint64_t poff_out = 0,
@@ -532,6 +533,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
 {
   static_assert(R == 8 || R == 16, "8- or 16-row tiles");
   static_assert(!PAIR || (!DEC && !FULL), "pairing is an encode mode for short symbols");
+  static_assert(!SL || (!DEC && FULL && !PAIR), "pre-sliced sources: whole spans of an encode / combine");
   static_assert(kBsRing == 4, "the unrolled loop assumes a 4-slot ring");
 #ifdef NTC_ABL_KLATE       // timing-only experiment builds: the late source read for every 16-row tile
   constexpr bool kLate = R == 16;
@@ -616,7 +618,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
 #pragma unroll
       for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
 #ifndef NTC_ABL_NOFILL     // timing-only ablation builds (tools/build_variant.sh -DNTC_ABL_...)
-      transpose8(Y);
+      if constexpr (!SL) transpose8(Y);                // SL: bs_preslice already sliced the source
 #endif
 #ifdef NTC_ABL_FILL2       // timing-only: a second transpose of the same source, results discarded
       {
@@ -736,7 +738,7 @@ __device__ __forceinline__ void bs_tile(const MacArgs& a, uint32_t g, uint32_t t
 // One wave per (generation, R-row tile, 2 KiB column span).  Blocks are renumbered so that each
 // XCD (block b runs on XCD b % 8) owns a contiguous range of tasks: the row tiles of one
 // generation then share that XCD's L2 instead of each pulling the sources from HBM.
-template <int R, bool DEC, bool FULL, bool PAIR = false>
+template <int R, bool DEC, bool FULL, bool PAIR = false, bool SL = false>
 __global__ __launch_bounds__(64 * kBsWaves)
 __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
 {
@@ -774,14 +776,14 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
   const uint32_t ring = lds_addr(s_ring + wave * (kBsRing * kBsSlot));
   if (!DEC && !PAIR && a.ksplit > 1) {
     const uint32_t i0 = ks * a.kpart;                  // launch_mac: every part is non-empty
-    bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring, 0, 0, i0, min(a.kpart, a.k - i0),
-                          ks ? a.kout + (ks - 1) * a.kout_step : a.out);
+    bs_tile<R, DEC, FULL, false, SL>(a, g, tile, nrows, cc, lane, ring, 0, 0, i0, min(a.kpart, a.k - i0),
+                                     ks ? a.kout + (ks - 1) * a.kout_step : a.out);
   } else if constexpr (PAIR) {
     const uint32_t pf = uniform(static_cast<uint32_t>(a.pair[g]));
     if (pf == 2) return;                               // encoded by its partner's wave
     bs_tile<R, DEC, FULL, true>(a, g, tile, nrows, cc, lane, ring, pf ? a.pair_in : 0, pf ? a.pair_out : 0);
   } else {
-    bs_tile<R, DEC, FULL>(a, g, tile, nrows, cc, lane, ring);
+    bs_tile<R, DEC, FULL, false, SL>(a, g, tile, nrows, cc, lane, ring);
   }
 }
 
@@ -2680,6 +2682,32 @@ __global__ __launch_bounds__(256) void ksplit_reduce(uint4* __restrict__ out, co
   }
 }
 
+// Bit-slice every 2 KiB span of a contiguous source block (stride % 2048 == 0) exactly as bs_tile's
+// fill does in registers: lane l's pieces [16 l, +16) and [1024 + 16 l, +16) of a span become the
+// 8 planes of transpose8, stored back in the same places, so gf_mac_bs<..., SL> loads planes
+// where it loaded bytes.  One HBM pass (n bytes read, n written) in place of the 48-op transpose
+// of every (source, 16-row tile) -- worth it once a source feeds many tiles (kSliceRows).
+// n32 = bytes / 32: one (span, lane) item per thread and step, 1 KiB contiguous per wave access.
+__global__ __launch_bounds__(256) void bs_preslice(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                   uint64_t n32)
+{
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * 256u;
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x; t < n32; t += step) {
+    const uint64_t i0 = (t >> 6) * 128u + (t & 63u);
+    const uint4 p = in[i0], q = in[i0 + 64];
+    uint32_t y[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+    transpose8(y);
+    out[i0] = make_uint4(y[0], y[1], y[2], y[3]);
+    out[i0 + 64] = make_uint4(y[4], y[5], y[6], y[7]);
+  }
+}
+
+// Rows from which an encode / combine with whole spans pre-slices its sources.  Measured at
+// config 5 (k = n = 1024, 64 KiB, profiles/r05/ab/preslice_config5.txt): the pass takes 0.025 ms
+// for 64 MiB (0.76 ns per 2 KiB span) and each MAC drops 0.874 -> 0.776 ms over 64 row tiles
+// (0.047 ns per span and 16-row tile), so it breaks even at ~16 tiles; 24 tiles keep a margin.
+constexpr uint32_t kSliceRows = 384;
+
 // Launch the region MAC over all (generation, row tile, column span) tasks of `a`.
 int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const char* what)
 {
@@ -2698,6 +2726,29 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     if (!a.pair && rowtile == 16 && e->mac_kind == NTC_GF256_MAC_BITSLICE_GROUPED && a.rows > 16) {
       group = 2;                                // gf_mac_bsg: tile pairs share the source fill
       fn = pick_bsg(dec, a.stride % 2048 == 0);
+    }
+    // a tall encode / combine over whole spans: slice the sources once (bs_preslice) instead of
+    // once per row tile
+    if (!dec && !a.pair && rowtile == 16 && group == 1 && a.stride % 2048 == 0 &&
+        (e->slice_force >= 0 ? e->slice_force != 0 : a.rows >= kSliceRows)) {
+      const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.stride;
+      // as for the split-k parts: a stream being captured must not allocate (then run unsliced)
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      const bool capturing = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+      if (n <= e->slice_cap || !capturing) {
+        int rc = ensure_buf(&e->slice, &e->slice_cap, n, "hipMalloc sliced sources");
+        if (rc) return rc;
+        const uint64_t n32 = n / 32;
+        const uint32_t nblk = static_cast<uint32_t>(std::min<uint64_t>((n32 + 255) / 256, 16384));
+        {
+          KernelTimer kt(e, NTC_GF256_K_SLICE, st, true);
+          hipExtLaunchKernelGGL(bs_preslice, dim3(nblk), dim3(256), 0, st, kt.start(), kt.stop(), 0,
+                                reinterpret_cast<const uint4*>(a.in0), static_cast<uint4*>(e->slice), n32);
+        }
+        if ((rc = hip_check(hipGetLastError(), "bs_preslice launch"))) return rc;
+        a.in0 = static_cast<const uint8_t*>(e->slice);
+        fn = gf_mac_bs<16, false, true, false, true>;
+      }
     }
     if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBsRing);
@@ -2907,6 +2958,10 @@ int ntc_gf256_engine_create(int device, ntc_gf256_engine** out)
     const int v = std::atoi(t);
     if (v >= 1 && v <= 8) e->ksplit_force = static_cast<uint32_t>(v);
   }
+  if (const char* t = std::getenv("NTC_GF256_SLICE")) {
+    if (!std::strcmp(t, "0")) e->slice_force = 0;
+    else if (!std::strcmp(t, "1")) e->slice_force = 1;
+  }
   if (const char* t = std::getenv("NTC_GF256_ROWTILE")) {
     if (!std::strcmp(t, "8")) e->rowtile_force = 8;
     else if (!std::strcmp(t, "16")) e->rowtile_force = 16;
@@ -2931,6 +2986,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->enc_coef);
   (void)hipFree(e->enc_pair);
   (void)hipFree(e->kout);
+  (void)hipFree(e->slice);
   (void)hipFree(e->row_ptr);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
   for (auto& pair : e->mac_ev)

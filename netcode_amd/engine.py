@@ -110,7 +110,7 @@ class Engine:
                       "ntc_gf256_set_plan_kind")
 
     KERNEL_KINDS = ("encode_prep", "encode_mac", "decode_plan", "plan_rows", "decode_mac",
-                    "bj_offsets", "dense", "other")
+                    "bj_offsets", "dense", "other", "preslice")
 
     def timing_log(self, capacity: int, kinds=None):
         """Bracket each of the next `capacity` kernel launches with HIP events (0 = off);

@@ -111,6 +111,10 @@ ENCODE_CASES = [
     # second ragged); uint32-wrapping ids and unequal lengths (one size product per source)
     (3, 37, 300, 1024, 1024, True, "wrap"),
     (2, 64, 513, 512, 512, False, "offset"),
+    # >= 384 rows over whole 2 KiB spans: sources pre-sliced once (bs_preslice + the SL MAC); a
+    # ragged last row tile, and split-k parts reading the sliced copy
+    (2, 37, 400, 2048, 2048, True, "wrap"),
+    (1, 130, 390, 4096, 4096, False, "offset"),
     # tile-pair workgroups (gf_mac_bsg, > 16 rows): k below the group size (wave 1 builds no
     # source, or one), partial spans with a short k, a second group with one idle wave
     (4, 1, 24, 2048, 2048, True, "offset"),

@@ -4,7 +4,8 @@
 #   steps: tests (pytest -m gpu), dense (test_gpu_dense.py only), mb (tools/mb_issue),
 #          bench (default bench line), c2|c4|c5 (per-config lines), smoke, batch (adaptor
 #          tests), pp (per-packet line), ppprof / ppsamp (flush / sampling profiles), c4pmc,
-#          surface, gatherab / gfwab (A/B against $AB_OTHER), ksplit (config-5 sweep)
+#          surface, gatherab / gfwab (A/B against $AB_OTHER), ksplit (config-5 sweep),
+#          slice (config 5 with / without pre-sliced sources)
 #   round-end evidence: tools/gpu_final_r05.sh
 set -o pipefail
 TAG=$1; STEPS=$2; shift 2
@@ -59,6 +60,12 @@ for s in "${S[@]}"; do
     ksplit)    # config-5 split-k part counts ($KS, default "3 4 5 6"), two interleaved reps
       for rep in 1 2; do for k in ${KS:-3 4 5 6}; do
         NTC_GF256_KSPLIT=$k run ks${k}_$rep 300 python bench.py --config k1024dense --no-cpu-baseline --no-host-rate
+      done; done ;;
+    slice)     # config 5 with / without pre-sliced sources (NTC_GF256_SLICE), two interleaved reps,
+               # after the tall-encode parity cases and the dense tests
+      run slice_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dense.py -x -q -m gpu -k "400 or 390 or dense" --timeout 240 --timeout-method thread
+      for rep in 1 2; do for v in 0 1; do
+        NTC_GF256_SLICE=$v run slice${v}_$rep 300 python bench.py --config k1024dense --no-cpu-baseline --no-host-rate
       done; done ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_shapes.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -2729,7 +2729,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     }
     // a tall encode / combine over whole spans: slice the sources once (bs_preslice) instead of
     // once per row tile
-    if (!dec && !a.pair && rowtile == 16 && group == 1 && a.stride % 2048 == 0 &&
+    if (!dec && !a.pair && group == 1 && a.stride % 2048 == 0 &&
         (e->slice_force >= 0 ? e->slice_force != 0 : a.rows >= kSliceRows)) {
       const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.stride;
       // as for the split-k parts: a stream being captured must not allocate (then run unsliced)
@@ -2747,7 +2747,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
         }
         if ((rc = hip_check(hipGetLastError(), "bs_preslice launch"))) return rc;
         a.in0 = static_cast<const uint8_t*>(e->slice);
-        fn = gf_mac_bs<16, false, true, false, true>;
+        fn = rowtile == 16 ? gf_mac_bs<16, false, true, false, true> : gf_mac_bs<8, false, true, false, true>;
       }
     }
     if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)

@@ -10,7 +10,8 @@ operand banks are controlled:
   b2    : two of the three sources share a bank
   same  : all three sources in one bank
 Forms: v_bitop3_b32 (XOR3), v_xor_b32_e32, v_fma_f32 (control), the same under
-s_set_gpr_idx_on (SRC0,DST), and v_bitop3 with an SGPR operand.  Each wave stamps s_memtime /
+s_set_gpr_idx_on (SRC0,DST), v_bitop3 with an SGPR operand, and scalar ops (alone and
+alternating with plain VALU in one wave: the decode plan's selector arithmetic).  Each wave stamps s_memtime /
 s_memrealtime around its loop (vector stores only), so cycles per instruction per SIMD =
 shader cycles / (waves per SIMD x instructions per wave), at the clock the chip actually held.
 
@@ -98,6 +99,15 @@ def body(form, banks, idx=False):
             out.append(f"v_bitop3_b32 v{a}, v{a}, 7, v{o1} bitop3:0x96")
         elif form == "readlane":
             out.append(f"v_readlane_b32 s{42 + n % 8}, v{o1}, {n % 64}")
+        elif form == "salu_lit":      # scalar AND with a literal (the plan's selector masks)
+            out.append(f"s_and_b32 s{42 + n % 8}, s{42 + (n + 3) % 8}, 0x7070707")
+        elif form == "salu_ss":       # scalar XOR of two SGPRs
+            out.append(f"s_xor_b32 s{42 + n % 8}, s{42 + n % 8}, s{42 + (n + 1) % 8}")
+        elif form == "salu_valu":     # one scalar and one plain VALU op alternating (same wave)
+            if n % 2:
+                out.append(f"s_xor_b32 s{42 + n % 8}, s{42 + n % 8}, s{42 + (n + 1) % 8}")
+            else:
+                out.append(f"v_bitop3_b32 v{a}, v{a}, v{o1}, v{o2} bitop3:0x96")
         elif form == "bitop3c":       # bitop3 with an inline-constant operand
             out.append(f"v_bitop3_b32 v{a}, v{a}, v{o1}, 7 bitop3:0x96")
     if idx:
@@ -220,6 +230,9 @@ VARIANTS = [
     ("shl3_c", "shl3", "cf", False),
     ("shl2_c", "shl2", "cf", False),
     ("bitop3c", "bitop3c", "cf", False),
+    ("salu_lit", "salu_lit", "cf", False),
+    ("salu_ss", "salu_ss", "cf", False),
+    ("salu_valu", "salu_valu", "cf", False),
     ("lanechain_noidx", "lane", "cf", False),
     ("lanechain_idx", "lane", "cf", True),
 ]

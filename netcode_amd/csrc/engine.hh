@@ -62,6 +62,11 @@ struct ntc_gf256_engine {
   void* dn_flag = nullptr; size_t dn_flag_cap = 0;
   void* dn_coef = nullptr; size_t dn_coef_cap = 0;
   void* dn_ok = nullptr;  size_t dn_ok_cap = 0;
+  // Graph capture: once any launch of this engine has been captured (KernelTimer notes it), a
+  // growing workspace buffer is retired here instead of freed -- a captured graph keeps the old
+  // address -- and released with the engine.
+  bool captured_any = false;
+  std::vector<void*> retired;
 };
 
 namespace ntcgpu {
@@ -70,8 +75,11 @@ namespace ntcgpu {
 int fail(int code, const std::string& msg);
 // NTC_GPU_OK, or the mapped status with the HIP error text recorded.
 int hip_check(hipError_t e, const char* what);
-// Grow a device buffer to at least `need` bytes (contents not preserved).
-int ensure_buf(void** p, size_t* cap, size_t need, const char* what);
+// Grow a device buffer of engine `e` to at least `need` bytes (contents not preserved; the old
+// buffer is freed, or retired if a graph may hold it: captured_any).
+int ensure_buf(ntc_gf256_engine* e, void** p, size_t* cap, size_t need, const char* what);
+// Release a workspace buffer that is being replaced (freed, or retired after a capture).
+void drop_buf(ntc_gf256_engine* e, void* p);
 // Coefficient rows padded to the MAC kernels' row tile (ntc_gf256_coef_pitch).
 uint32_t tile_rp(uint32_t r);
 
@@ -85,6 +93,13 @@ class KernelTimer {
   KernelTimer(ntc_gf256_engine* e, uint32_t kind, hipStream_t st, bool ext = false)
       : e_(e), st_(st), ext_(ext)
   {
+    // every launch region passes here: note a graph capture (the null stream is never captured,
+    // so the default-stream case costs no runtime call)
+    if (!e_->captured_any && st_ != nullptr) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st_, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        e_->captured_any = true;
+    }
     if (e_->tlog_n < e_->tlog_cap && ((e_->tlog_mask >> kind) & 1u)) {
       slot_ = static_cast<int>(e_->tlog_n++);
       e_->tlog_kind[slot_] = kind;

@@ -768,12 +768,12 @@ int dense_invert(ntc_gf256_engine* e, uint32_t G, uint32_t n, const uint8_t* mat
   const uint32_t np = (n + kPanel - 1) / kPanel * kPanel;
   const size_t xb = static_cast<size_t>(G) * np * 2 * np;
   int rc;
-  if ((rc = ensure_buf(&e->dn_x, &e->dn_x_cap, xb, "hipMalloc dense X"))) return rc;
-  if ((rc = ensure_buf(&e->dn_y, &e->dn_y_cap, xb, "hipMalloc dense Y"))) return rc;
-  if ((rc = ensure_buf(&e->dn_w, &e->dn_w_cap, static_cast<size_t>(G) * kPanel * np + 16, "hipMalloc dense W"))) return rc;
-  if ((rc = ensure_buf(&e->dn_piv, &e->dn_piv_cap, static_cast<size_t>(G) * np * 4 + 16, "hipMalloc dense piv"))) return rc;
-  if ((rc = ensure_buf(&e->dn_flag, &e->dn_flag_cap, static_cast<size_t>(G) * np * 3 + 16, "hipMalloc dense flags"))) return rc;
-  if ((rc = ensure_buf(&e->dn_ok, &e->dn_ok_cap, G + 16, "hipMalloc dense ok"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_x, &e->dn_x_cap, xb, "hipMalloc dense X"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_y, &e->dn_y_cap, xb, "hipMalloc dense Y"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_w, &e->dn_w_cap, static_cast<size_t>(G) * kPanel * np + 16, "hipMalloc dense W"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_piv, &e->dn_piv_cap, static_cast<size_t>(G) * np * 4 + 16, "hipMalloc dense piv"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_flag, &e->dn_flag_cap, static_cast<size_t>(G) * np * 3 + 16, "hipMalloc dense flags"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_ok, &e->dn_ok_cap, G + 16, "hipMalloc dense ok"))) return rc;
   uint8_t* X = static_cast<uint8_t*>(e->dn_x);
   uint8_t* Y = static_cast<uint8_t*>(e->dn_y);
   uint8_t* flag = static_cast<uint8_t*>(e->dn_flag);
@@ -880,7 +880,7 @@ int ntc_gf256_dense_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, ui
   (void)hipSetDevice(e->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint32_t pitch = ntc_gf256_coef_pitch(r);
-  int rc = ensure_buf(&e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * k * pitch + 64, "hipMalloc dense coef");
+  int rc = ensure_buf(e, &e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * k * pitch + 64, "hipMalloc dense coef");
   if (rc) return rc;
   // combine wants coef[g][i][j] (input-major): the transpose of mat[g][j][i]
   {
@@ -916,7 +916,7 @@ int ntc_gf256_dense_decode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t n, ui
   hipLaunchKernelGGL(dn_gather_inv, dim3(n, G), dim3(256), 0, st, n, np, X,
                      static_cast<const uint32_t*>(e->dn_piv), static_cast<const uint8_t*>(e->dn_ok), invbuf);
   if ((rc = hip_check(hipGetLastError(), "dn_gather_inv launch"))) return rc;
-  if ((rc = ensure_buf(&e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * n * pitch + 64, "hipMalloc dense coef"))) return rc;
+  if ((rc = ensure_buf(e, &e->dn_coef, &e->dn_coef_cap, static_cast<size_t>(G) * n * pitch + 64, "hipMalloc dense coef"))) return rc;
   hipLaunchKernelGGL(dn_transpose, dim3((n + 63) / 64, (pitch + 63) / 64, G), dim3(256), 0, st, n, n,
                      pitch, invbuf, static_cast<uint8_t*>(e->dn_coef));
   if ((rc = hip_check(hipGetLastError(), "dn_transpose launch"))) return rc;

@@ -2736,7 +2736,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool capturing = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
       if (n <= e->slice_cap || !capturing) {
-        int rc = ensure_buf(&e->slice, &e->slice_cap, n, "hipMalloc sliced sources");
+        int rc = ensure_buf(e, &e->slice, &e->slice_cap, n, "hipMalloc sliced sources");
         if (rc) return rc;
         const uint64_t n32 = n / 32;
         const uint32_t nblk = static_cast<uint32_t>(std::min<uint64_t>((n32 + 255) / 256, 16384));
@@ -2752,7 +2752,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     }
     if (dec && !a.row_ptr) {                   // (else the plan wrote the row addresses)
       const uint64_t nr = static_cast<uint64_t>(a.G) * (a.k + kBsRing);
-      int rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
+      int rc = ensure_buf(e, &e->row_ptr, &e->row_ptr_cap, nr * 8, "hipMalloc row_ptr");
       if (rc) return rc;
       // row_ptr now holds these buffers' addresses, not those a plan recorded
       e->rows_src = nullptr;
@@ -2816,7 +2816,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     }
   }
   if (a.ksplit > 1) {
-    int rc = ensure_buf(&e->kout, &e->kout_cap, (a.ksplit - 1) * a.kout_step, "hipMalloc split-k parts");
+    int rc = ensure_buf(e, &e->kout, &e->kout_cap, (a.ksplit - 1) * a.kout_step, "hipMalloc split-k parts");
     if (rc) return rc;
     a.kout = static_cast<uint8_t*>(e->kout);
     tasks *= a.ksplit;
@@ -2859,10 +2859,17 @@ uint32_t tile_rp(uint32_t r)
   return round_up(r, 32);
 }
 
-int ensure_buf(void** p, size_t* cap, size_t need, const char* what)
+void drop_buf(ntc_gf256_engine* e, void* p)
+{
+  if (!p) return;
+  if (e->captured_any) e->retired.push_back(p);   // a captured graph may still address it
+  else (void)hipFree(p);
+}
+
+int ensure_buf(ntc_gf256_engine* e, void** p, size_t* cap, size_t need, const char* what)
 {
   if (need <= *cap) return NTC_GPU_OK;
-  (void)hipFree(*p);
+  drop_buf(e, *p);
   *p = nullptr;
   *cap = 0;
   int rc = hip_check(hipMalloc(p, need), what);
@@ -2882,10 +2889,10 @@ int ensure_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t rp)
   const size_t nk = k > e->plan_cap_k ? k : e->plan_cap_k;
   const size_t nrp = rp > e->plan_cap_rp ? rp : e->plan_cap_rp;
   (void)hipSetDevice(e->device);
-  (void)hipFree(e->plan_m);
-  (void)hipFree(e->plan_in);
-  (void)hipFree(e->plan_out);
-  (void)hipFree(e->plan_coef);
+  drop_buf(e, e->plan_m);
+  drop_buf(e, e->plan_in);
+  drop_buf(e, e->plan_out);
+  drop_buf(e, e->plan_coef);
   e->plan_m = nullptr; e->plan_in = nullptr; e->plan_out = nullptr; e->plan_coef = nullptr;
   e->plan_cap_G = e->plan_cap_k = e->plan_cap_rp = 0;
   int rc;
@@ -2989,6 +2996,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* e)
   (void)hipFree(e->slice);
   (void)hipFree(e->row_ptr);
   for (void* b : {e->dn_x, e->dn_y, e->dn_w, e->dn_piv, e->dn_flag, e->dn_coef, e->dn_ok}) (void)hipFree(b);
+  for (void* b : e->retired) (void)hipFree(b);
   for (auto& pair : e->mac_ev)
     for (hipEvent_t ev : pair)
       if (ev) (void)hipEventDestroy(ev);
@@ -3089,11 +3097,11 @@ int ntc_gf256_reserve(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r)
   if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
   (void)hipSetDevice(e->device);
   const uint32_t rp = tile_rp(r);
-  int rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+  int rc = ensure_buf(e, &e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   if (rc) return rc;
-  if ((rc = ensure_buf(&e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair"))) return rc;
+  if ((rc = ensure_buf(e, &e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair"))) return rc;
   // the decode MAC's input row addresses (decode_plan_w / plan_rows), so later calls never allocate
-  if ((rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<size_t>(G) * (k + kBsRing) * 8,
+  if ((rc = ensure_buf(e, &e->row_ptr, &e->row_ptr_cap, static_cast<size_t>(G) * (k + kBsRing) * 8,
                        "hipMalloc row_ptr")))
     return rc;
   return ensure_plan(e, G, k, rp);
@@ -3111,7 +3119,7 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
   (void)hipSetDevice(e->device);
   const uint32_t rp = tile_rp(r);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  rc = ensure_buf(&e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
+  rc = ensure_buf(e, &e->enc_coef, &e->enc_coef_cap, static_cast<size_t>(G) * k * rp + 64, "hipMalloc enc_coef");
   if (rc) return rc;
   // generation pairing (kPairGap): symbols of at most half a bit-sliced span that fill at least a
   // third of it when paired; pays off with continuous ids.  Under AUTO, a stride the unpaired
@@ -3123,7 +3131,7 @@ int ntc_gf256_encode_batch(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t
                         (e->mac_kind == NTC_GF256_MAC_AUTO && 2u * stride * 100u >= 2048u * 33u &&
                          (use_bitslice(e, stride) || (!sid_base && !rid_base))));
   if (pairing &&
-      (rc = ensure_buf(&e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair")))
+      (rc = ensure_buf(e, &e->enc_pair, &e->enc_pair_cap, G, "hipMalloc enc_pair")))
     return rc;
   PrepArgs p{};
   p.G = G; p.k = k; p.r = r; p.rp = rp; p.src_len = src_len; p.sid_base = sid_base;
@@ -3175,7 +3183,7 @@ static int plan_impl(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t r, ui
   const bool lds_plan = kind == NTC_GF256_PLAN_LDS;
   const bool wave_plan = !big && r <= 32 && !lds_plan;
   if (wave_plan && rows_src && rows_rep && use_bitslice(e, rows_stride)) {
-    rc = ensure_buf(&e->row_ptr, &e->row_ptr_cap, static_cast<uint64_t>(G) * (k + kBsRing) * 8,
+    rc = ensure_buf(e, &e->row_ptr, &e->row_ptr_cap, static_cast<uint64_t>(G) * (k + kBsRing) * 8,
                     "hipMalloc row_ptr");
     if (rc) return rc;
     p.rows_out = static_cast<uint64_t*>(e->row_ptr);

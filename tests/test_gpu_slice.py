@@ -1,7 +1,8 @@
 """Sources bit-sliced once per call (bs_preslice + gf_mac_bs<..., SL>): a combine with >= 384 rows
 over whole 2 KiB spans slices its sources into an engine buffer first.  The buffer is sized on first
 use, so a call captured into a graph before that use must run unsliced (no allocation during
-capture) and one captured after it runs sliced -- both must equal the oracle's dense encode
+capture) and one captured after it runs sliced -- both must equal the oracle's dense encode,
+and the sliced graph must stay valid after a larger call has grown the buffer
 (oracle.dense_encode: rep[j] = sum_i mat[j][i] * src[i], the reference's region multiply_add,
 galois_field.hh:65-92)."""
 import ctypes as C
@@ -34,17 +35,20 @@ def test_tall_combine_sliced_under_graph_capture(gpu, oracle):
             _native.check(L.ntc_gf256_combine_batch(h, G, k, rows, stride, s_t.data_ptr(), c_t.data_ptr(),
                                                     out.data_ptr(), stream), "combine")
 
-        def captured():
+        def capture():
             out = torch.full((G, rows, stride), 0xA5, dtype=torch.uint8, device=gpu)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 combine(out, torch.cuda.current_stream(gpu).cuda_stream)
+            return graph, out
+
+        def replay(graph, out):
             out.fill_(0xA5)
             graph.replay()
             torch.cuda.synchronize(gpu)
             return out.cpu().numpy()
 
-        assert (captured() == ref).all()                       # before any sizing: unsliced
+        assert (replay(*capture()) == ref).all()               # before any sizing: unsliced
         out = torch.empty((G, rows, stride), dtype=torch.uint8, device=gpu)
         _native.check(L.ntc_gf256_timing_log(h, 8), "timing log")
         combine(out, torch.cuda.current_stream(gpu).cuda_stream)   # sizes the sliced copy
@@ -56,7 +60,19 @@ def test_tall_combine_sliced_under_graph_capture(gpu, oracle):
         assert list(kinds[:n.value]) == [8, 1]                 # NTC_GF256_K_SLICE, then the MAC
         torch.cuda.synchronize(gpu)
         assert (out.cpu().numpy() == ref).all()
-        assert (captured() == ref).all()                       # buffer present: sliced in the graph
+        sliced = capture()
+        assert (replay(*sliced) == ref).all()                  # buffer present: sliced in the graph
+        # a later, larger call grows the sliced copy: the old one must outlive the graph that
+        # addresses it (retired, not freed, once the engine has seen a capture)
+        big = torch.zeros((G, 2 * k, stride), dtype=torch.uint8, device=gpu)
+        big_c = torch.zeros((G, 2 * k, rp), dtype=torch.uint8, device=gpu)
+        big_o = torch.empty((G, rows, stride), dtype=torch.uint8, device=gpu)
+        _native.check(L.ntc_gf256_combine_batch(h, G, 2 * k, rows, stride, big.data_ptr(), big_c.data_ptr(),
+                                                big_o.data_ptr(), torch.cuda.current_stream(gpu).cuda_stream),
+                      "larger combine")
+        torch.cuda.synchronize(gpu)
+        assert not big_o.any()
+        assert (replay(*sliced) == ref).all()
     finally:
         torch.cuda.synchronize(gpu)
         L.ntc_gf256_engine_destroy(h)

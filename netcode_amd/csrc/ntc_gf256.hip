@@ -2732,12 +2732,22 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     if (!dec && !a.pair && group == 1 && a.stride % 2048 == 0 &&
         (e->slice_force >= 0 ? e->slice_force != 0 : a.rows >= kSliceRows)) {
       const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.stride;
-      // as for the split-k parts: a stream being captured must not allocate (then run unsliced)
+      // as for the split-k parts: a stream being captured must not allocate; and the copy is an
+      // optimisation, so without room for it (hipMalloc fails) the MAC slices in registers
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool capturing = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
-      if (n <= e->slice_cap || !capturing) {
-        int rc = ensure_buf(e, &e->slice, &e->slice_cap, n, "hipMalloc sliced sources");
-        if (rc) return rc;
+      if (n > e->slice_cap && !capturing) {
+        void* p = nullptr;
+        if (hipMalloc(&p, n) == hipSuccess) {
+          drop_buf(e, e->slice);
+          e->slice = p;
+          e->slice_cap = n;
+        } else {
+          (void)hipGetLastError();             // clear it: the call proceeds unsliced
+        }
+      }
+      if (n <= e->slice_cap) {
+        int rc;
         const uint64_t n32 = n / 32;
         const uint32_t nblk = static_cast<uint32_t>(std::min<uint64_t>((n32 + 255) / 256, 16384));
         {

@@ -2825,9 +2825,20 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       a.kpart = a.k;
     }
   }
+  if (a.ksplit > 1 && (a.ksplit - 1) * a.kout_step > e->kout_cap) {
+    // the split is an optimisation: without room for the parts the MAC runs unsplit
+    void* p = nullptr;
+    if (hipMalloc(&p, (a.ksplit - 1) * a.kout_step) == hipSuccess) {
+      drop_buf(e, e->kout);
+      e->kout = p;
+      e->kout_cap = (a.ksplit - 1) * a.kout_step;
+    } else {
+      (void)hipGetLastError();
+      a.ksplit = 1;
+      a.kpart = a.k;
+    }
+  }
   if (a.ksplit > 1) {
-    int rc = ensure_buf(e, &e->kout, &e->kout_cap, (a.ksplit - 1) * a.kout_step, "hipMalloc split-k parts");
-    if (rc) return rc;
     a.kout = static_cast<uint8_t*>(e->kout);
     tasks *= a.ksplit;
   }

@@ -119,7 +119,8 @@ int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uin
  * k >= 128) splits its sources (split-k) and sizes its partial outputs on first use; a call
  * captured before that first use runs unsplit instead of allocating (identical results).  The
  * pre-sliced source copy of a tall encode / combine is sized the same way (captured before its
- * first use: the MAC slices in registers instead).  Once any call of an engine has been captured,
+ * first use: the MAC slices in registers instead).  Both are optimisations: when the device has
+ * no room for them the call runs without them (identical results) instead of failing.  Once any call of an engine has been captured,
  * a workspace buffer that a later, larger call outgrows is kept (not freed) until the engine is
  * destroyed, so captured graphs never address freed memory. */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);

@@ -115,6 +115,7 @@ ENCODE_CASES = [
     # ragged last row tile, and split-k parts reading the sliced copy
     (2, 37, 400, 2048, 2048, True, "wrap"),
     (1, 130, 390, 4096, 4096, False, "offset"),
+    (2, 128, 400, 2048, 2048, True, "default"),       # two generations' parts in one sliced copy
     # tile-pair workgroups (gf_mac_bsg, > 16 rows): k below the group size (wave 1 builds no
     # source, or one), partial spans with a short k, a second group with one idle wave
     (4, 1, 24, 2048, 2048, True, "offset"),

@@ -23,6 +23,18 @@ def test_header_symbols_match_loader_list():
     assert _declared_symbols("gpu.h") == sorted(_native.GPU_H_SYMBOLS)
 
 
+def test_kernel_kind_names_match_header():
+    """The timing log's kinds (NTC_GF256_K_* in gpu.h) and the names the Python mirror and
+    bench.py give them (Engine.KERNEL_KINDS, indexed by value) stay in step."""
+    from netcode_amd.engine import Engine
+    txt = open(os.path.join(ROOT, "include", "netcode", "gpu.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    kinds = {int(v): n.lower() for n, v in re.findall(r"NTC_GF256_K_([A-Z_]+)\s*=\s*(\d+)", txt)}
+    assert sorted(kinds) == list(range(len(Engine.KERNEL_KINDS)))
+    alias = {"slice": "preslice"}
+    assert [alias.get(kinds[i], kinds[i]) for i in sorted(kinds)] == list(Engine.KERNEL_KINDS)
+
+
 def test_library_loads_and_exports(native_built):
     from netcode_amd import _native
     L = _native.load()

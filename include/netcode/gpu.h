@@ -68,10 +68,14 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
 
 /* Region-MAC formulation (tuning and A/B testing; results are identical).  AUTO picks the
  * bit-sliced XOR kernel when the stride fills >= 1/3 of its 2 KiB wave span (stride % 16 == 0),
- * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice|grouped environment variable
+ * the v_perm kernel otherwise; the NTC_GF256_MAC=perm|bitslice|grouped|paired environment variable
  * overrides AUTO process-wide.  BITSLICE runs one independent wave per row tile (gf_mac_bs);
  * BITSLICE_GROUPED (experimental, slower on MI355X: DESIGN.md §3) runs pairs of 16-row tiles per
- * workgroup that build each source's bit planes once and share them through LDS (gf_mac_bsg).
+ * workgroup that build each source's bit planes once and share them through LDS (gf_mac_bsg);
+ * BITSLICE_PAIRED (experimental, 1-3 % slower on MI355X: DESIGN.md §3) runs the two 16-row tiles
+ * of a (generation, span) as one 2-wave workgroup in which each wave transposes half the sources
+ * and publishes only their 8 planes to the other (gf_mac_bsp; NTC_GF256_MAC=paired, with
+ * NTC_GF256_PAIRJ=1|2 sources per wave and turn, NTC_GF256_PAIRSETS=3|4 LDS slot sets).
  * An encode / combine with >= 384 rows over whole 2 KiB spans (BITSLICE or AUTO) first bit-slices
  * its sources into an engine buffer (one HBM pass), so the MAC's row tiles skip the per-tile
  * transpose.  More environment variables, for experiments only (results identical):
@@ -79,7 +83,7 @@ void ntc_gf256_engine_destroy(ntc_gf256_engine* eng);
  * rows), NTC_GF256_KSPLIT=n (1..8) fixes the split-k part count of encodes with too few tasks to
  * fill the GPU, NTC_GF256_SLICE=0|1 turns the source pre-slicing off / on for every eligible call. */
 enum { NTC_GF256_MAC_AUTO = 0, NTC_GF256_MAC_PERM = 1, NTC_GF256_MAC_BITSLICE = 2,
-       NTC_GF256_MAC_BITSLICE_GROUPED = 3 };
+       NTC_GF256_MAC_BITSLICE_GROUPED = 3, NTC_GF256_MAC_BITSLICE_PAIRED = 4 };
 int  ntc_gf256_set_mac_kind(ntc_gf256_engine* eng, int kind);
 
 /* Decode-plan kernel (coverage and A/B testing; results are identical).  AUTO: the register-
@@ -120,10 +124,16 @@ int  ntc_gf256_timing_read(ntc_gf256_engine* eng, uint32_t max, uint32_t* n, uin
  * captured before that first use runs unsplit instead of allocating (identical results).  The
  * pre-sliced source copy of a tall encode / combine is sized the same way (captured before its
  * first use: the MAC slices in registers instead).  Both are optimisations: when the device has
- * no room for them the call runs without them (identical results) instead of failing.  Once any call of an engine has been captured,
- * a workspace buffer that a later, larger call outgrows is kept (not freed) until the engine is
- * destroyed, so captured graphs never address freed memory. */
+ * no room for them the call runs without them (identical results) instead of failing.  Once any
+ * call of an engine has been captured, a workspace buffer that a later, larger call outgrows is
+ * kept (not freed) until the engine is destroyed or ntc_gf256_release_retired is called, so
+ * captured graphs never address freed memory; from then on buffers grow at least 2x at a time,
+ * so the retired memory stays below the current workspace (split-k parts and the sliced copy are
+ * G * k * stride bytes scale: 64 MiB each at k = 1024, 64 KiB, G = 1). */
 int  ntc_gf256_reserve(ntc_gf256_engine* eng, uint32_t G, uint32_t k, uint32_t r);
+/* Free the workspace buffers retired after a capture.  Only once no graph captured from this
+ * engine will be launched again (e.g. after hipGraphExecDestroy of all of them). */
+int  ntc_gf256_release_retired(ntc_gf256_engine* eng);
 
 /* Encode: rep[g][j] = sum_i c(rid_base[g]+j, sid_base[g]+i) * src[g][i] over GF(2^8)/0x11D.
  * Any r (the coefficient walk runs in chunks of 256 rows); k <= 65535.

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("NTC_GF256_LIB") or os.path.join(HERE, "libntc_gf256.s
 # Every symbol include/netcode/gpu.h declares (tests check the .so exports all of them).
 GPU_H_SYMBOLS = [
     "ntc_gf256_engine_create", "ntc_gf256_engine_destroy", "ntc_gf256_set_mac_kind",
-    "ntc_gf256_reserve",
+    "ntc_gf256_reserve", "ntc_gf256_release_retired",
     "ntc_gf256_encode_batch", "ntc_gf256_decode_batch", "ntc_gf256_decode_plan",
     "ntc_gf256_decode_apply", "ntc_gf256_region_multiply", "ntc_gf256_coef_pitch",
     "ntc_gf256_combine_batch", "ntc_gf256_coefficient",
@@ -65,6 +65,7 @@ def load(path: str | None = None):
     L.ntc_gf256_engine_destroy.restype = None
     L.ntc_gf256_set_mac_kind.argtypes = [V, C.c_int]
     L.ntc_gf256_reserve.argtypes = [V, u32, u32, u32]
+    L.ntc_gf256_release_retired.argtypes = [V]
     L.ntc_gf256_encode_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, P, P, P, P, V]
     L.ntc_gf256_decode_batch.argtypes = [V, u32, u32, u32, u32, P, P, P, P, P, P, P, P, P, V]
     L.ntc_gf256_decode_plan.argtypes = [V, u32, u32, u32, P, P, P, P, P, P, P, V]

@@ -39,6 +39,8 @@ struct ntc_gf256_engine {
   void* row_ptr = nullptr;     // bit-sliced decode: input row address per plan position
   size_t row_ptr_cap = 0;
   int mac_kind = NTC_GF256_MAC_AUTO;
+  int pair_j = 2;                   // gf_mac_bsp sources per wave and turn (NTC_GF256_PAIRJ)
+  int pair_sets = 3;                // gf_mac_bsp slot sets, 3 or 4 (NTC_GF256_PAIRSETS)
   uint32_t rowtile_force = 0;  // bit-sliced row tile 8 or 16 (NTC_GF256_ROWTILE; 0 = by rows)
   uint32_t ksplit_force = 0;   // split-k part count 1..8 (NTC_GF256_KSPLIT; 0 = the heuristic)
   int slice_force = -1;        // pre-sliced sources 0 / 1 (NTC_GF256_SLICE; -1 = by rows)
@@ -80,6 +82,9 @@ int hip_check(hipError_t e, const char* what);
 int ensure_buf(ntc_gf256_engine* e, void** p, size_t* cap, size_t need, const char* what);
 // Release a workspace buffer that is being replaced (freed, or retired after a capture).
 void drop_buf(ntc_gf256_engine* e, void* p);
+// Allocation size for a workspace buffer of capacity cap that must hold need bytes (doubling once
+// any launch has been captured, so that few outgrown buffers are retired).
+size_t grow_to(const ntc_gf256_engine* e, size_t need, size_t cap);
 // Coefficient rows padded to the MAC kernels' row tile (ntc_gf256_coef_pitch).
 uint32_t tile_rp(uint32_t r);
 

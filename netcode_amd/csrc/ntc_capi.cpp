@@ -446,6 +446,8 @@ class Device {
     // a staging set with no flight in it (else wait for the oldest flight)
     int si = !st_[0].busy ? 0 : !st_[1].busy ? 1 : -1;
     if (si < 0) {
+      // a busy set always has its flight queued (complete_oldest_locked); checked all the same
+      if (flights_.empty()) throw device_error("batch staging sets busy with no flight queued");
       si = flights_.front().set;
       complete_oldest_locked();
     }
@@ -582,17 +584,20 @@ class Device {
 
   // the oldest flight: wait for its work, then its roots' values into the nodes (a copy out of
   // pinned memory: reading the pinned results in place at every use measured slower)
+  // If the wait fails (it throws), the flight stays queued and its staging set stays busy: the
+  // queue and the sets never disagree, and a later call waits for the same flight again.
   void complete_oldest_locked()
   {
     NTC_PROF_T(t_c);
-    Flight f = std::move(flights_.front());
-    flights_.pop_front();
-    Stage& S = st_[f.set];
+    Stage& S = st_[flights_.front().set];
     {
       NTC_PROF_T(t_wait);
       wait_event(S.ev);
       NTC_PROF_ADD(wait, t_wait);
     }
+    Flight f = std::move(flights_.front());
+    flights_.pop_front();
+    S.busy = false;
     for (const NodeRef& n : f.todo) n->expr.clear();
     for (auto& rp : f.roots) {
       Node* r = rp.first.get();
@@ -601,7 +606,6 @@ class Device {
       r->hoff = 0;
       r->fetched = true;
     }
-    S.busy = false;
     NTC_PROF_ADD(complete, t_c);
   }
 

@@ -787,6 +787,283 @@ __attribute__((amdgpu_waves_per_eu(R == 16 ? 3 : 4))) void gf_mac_bs(MacArgs a)
   }
 }
 
+// ---- paired bit-sliced MAC: the two 16-row tiles of a (generation, span) share the transpose ----
+// The 48-op 8x8 bit transpose of a source depends only on the source, yet every 16-row tile of a
+// generation repeated it (≈ 17-19 of the ≈ 66 cycles per row and source).  Here a
+// 2-wave workgroup holds tiles 2p and 2p+1 of one (generation, 2 KiB span).  Sources go in turns of
+// TS = 2J; in turn T wave w owns sources T*TS + 2j + w (j < J): it LDS-DMAs them two turns ahead,
+// transposes each from its raw slot, publishes the 8 planes in that same slot and runs its own
+// chain on them at once; its partner reads those planes one turn later.  Each wave transposes half
+// the sources and builds its own 22 plane tables (NTC_BS_TABLES) from all of them -- only the
+// 8 planes cross LDS (2 KiB, the bytes the raw source already occupies), unlike gf_mac_bsg's 30.
+// Per turn, one barrier, placed before the last partner step:
+//   own(T,0) partner(T-1,0) ... own(T,J-1) | barrier, DMA turn T+NS-1 | partner(T-1,J-1)
+// It certifies that both waves published turn T's planes (read in turn T+1) and both finished
+// reading turn T-1's, whose slots then take turn T+NS-1's DMA: NS slot sets of TS slots.  XOR is
+// order-free, so the two waves summing the sources in different orders changes no byte.  Every
+// LDS read -- raw bytes of an own source, planes of a partner source -- is issued one step ahead,
+// into the ycur registers, as in bs_tile.
+template <int J, int NS, bool DEC, bool FULL, uint32_t w>
+__device__ __forceinline__ void bs_pair(const MacArgs& a, uint32_t g, uint32_t tile, uint32_t nrows,
+                                        uint32_t cc, uint32_t lane, uint32_t ring)
+{
+  // w (the wave of the pair) is a template argument: own and partner slots are then immediate
+  // offsets from one address register
+  constexpr uint32_t TS = 2 * J;                       // sources per turn
+  constexpr uint32_t kSet = TS * kBsSlot;              // LDS bytes of one turn's slots
+  const size_t stride = a.stride;
+  const uint32_t k = a.k;
+  const uint32_t col = cc * 2048u;
+  const uint32_t x = ring + lane * 16u;
+  const bool v0 = FULL || col + lane * 16u < stride;
+  const bool v1 = FULL || col + lane * 16u + 1024u < stride;
+  const uint8_t* base0 = a.in0 + static_cast<size_t>(g) * k * stride;
+  const uint64_t* rowp = DEC ? a.row_ptr + static_cast<size_t>(g) * (k + kBsRing) : nullptr;
+  const uint8_t* jp0 = a.coef + static_cast<size_t>(g) * k * a.rp + tile * 16u;
+  const uint32_t rp = a.rp;
+  const uint64_t bias = static_cast<uint64_t>(col) - ring;
+  const uint32_t nT = (k + TS - 1) / TS;
+  auto row_at = [&](uint32_t i) -> const uint8_t* {    // scalar row address of source min(i, k-1)
+    i = i < k ? i : k - 1;
+    uint64_t v;
+    if constexpr (DEC) v = const_load<uint64_t>(rowp + i);
+    else v = reinterpret_cast<uint64_t>(base0 + static_cast<size_t>(i) * stride);
+    const uint32_t lo = uniform(static_cast<uint32_t>(v)), hi = uniform(static_cast<uint32_t>(v >> 32));
+    return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  auto coef_at = [&](uint32_t i) __attribute__((always_inline)) {   // zero past k: the chain returns at once
+    return i < k ? const_load<u32x4>(jp0 + static_cast<size_t>(i) * rp) : u32x4{0, 0, 0, 0};
+  };
+  static_assert(NS == 3 || NS == 4, "3 or 4 slot sets");
+  auto set_of = [](uint32_t T) { return (T % NS) * kSet; };   // LDS offset of turn T's slots
+  // x is kept in v0 at every LDS access: with 128 accumulators, 30 table planes and the 8 ycur
+  // registers only v0 / v1 are left, and the allocator otherwise spills x to make room for the
+  // transpose's temporaries
+  auto xv0 = [&]() __attribute__((always_inline)) {
+    uint32_t v = x;
+    asm volatile("" : "+{v0}"(v));
+    return v;
+  };
+  // this wave's J sources of turn T into their slots (sources past k: the last one again, so every
+  // turn issues 2J DMAs and the vmcnt arithmetic below holds)
+  auto issue_turn = [&](uint32_t T) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint8_t* row = row_at(T * TS + 2 * j + w) + bias;
+      const uint32_t m0 = uniform(ring + set_of(T) + (2 * j + w) * kBsSlot);
+      uint32_t keep;
+      if constexpr (FULL) {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, %2\n\t"
+                     "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(x), "s"(row), "s"(m0) : "memory");
+      } else {
+        // clamped offsets (loaded, never stored), formed here from an opaque copy of x so that
+        // they are not kept live across the loop
+        const uint32_t xx = xv0();
+        const uint32_t d0 = v0 ? xx : ring, d1 = v1 ? xx + 1024u : ring;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, %3\n\t"
+                     "s_add_u32 m0, %4, 0x400\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %2, %3\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(d0), "v"(d1), "s"(row), "s"(m0) : "memory", "scc");
+      }
+    }
+  };
+  // before reading own source j of turn T': the DMAs issued after it are the turn's later own
+  // sources and the turns after T' issued so far -- up to T' + NS - 2 (at most nT)
+  auto wait_own = [&](int j, uint32_t Tp) __attribute__((always_inline)) {
+    const uint32_t na = Tp + (NS - 2) <= nT ? NS - 2 : (Tp <= nT ? nT - Tp : 0u);
+    const int base = 2 * (J - 1 - j);
+    if (na == 0) { if (base == 0) vm_wait<0>(); else vm_wait<2>(); }
+    else if (na == 1) { if (base == 0) vm_wait<2 * J>(); else vm_wait<2 + 2 * J>(); }
+    else { if (base == 0) vm_wait<4 * J>(); else vm_wait<2 + 4 * J>(); }
+  };
+  auto lds_read = [&](uint32_t off, uint32_t (&y)[8]) __attribute__((always_inline)) {
+    const auto* p = reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(xv0() + off);
+    const u32x4 q0 = p[0], q1 = p[1024 / 16];
+    y[0] = q0[0]; y[1] = q0[1]; y[2] = q0[2]; y[3] = q0[3];
+    y[4] = q1[0]; y[5] = q1[1]; y[6] = q1[2]; y[7] = q1[3];
+  };
+  auto lds_write = [&](uint32_t off, const uint32_t* y) __attribute__((always_inline)) {
+    auto* p = reinterpret_cast<__attribute__((address_space(3))) u32x4*>(xv0() + off);
+    p[0] = u32x4{y[0], y[1], y[2], y[3]};
+    p[1024 / 16] = u32x4{y[4], y[5], y[6], y[7]};
+  };
+#ifndef NTC_ABL_NOBARRIER
+  auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+#else                      // timing-only ablation (wrong results): no synchronisation of the pair
+  auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+#endif
+
+  u32x8 A[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) A[j] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t tbase = bs_table_base();
+  auto chain = [&](const u32x4& o, uint32_t (&Y)[kBsPlanes]) __attribute__((always_inline)) {
+    uint64_t P0 = (static_cast<uint64_t>(o[1]) << 32) | o[0];
+    uint64_t P1 = (static_cast<uint64_t>(o[3]) << 32) | o[2];      // rows 8-15: s[88:89]
+    asm volatile("s_mov_b32 s94, m0\n" NTC_BS_ENTER NTC_BS_LEAVE
+                 : NTC_BS_OUTS16(A), [p] "+{s[90:91]}"(P0), [q] "+{s[88:89]}"(P1)
+                 : NTC_BS_YPINS(Y), [tb] "{s[96:97]}"(tbase)
+                 : NTC_BS_CLOB);
+  };
+
+  uint32_t ycur[8];
+  u32x4 on;
+  // own step: ycur = the raw bytes -> transpose -> publish the planes at `wr` -> issue the next
+  // step's read -> tables -> chain.  Partner step: ycur = the planes -> next read -> tables -> chain.
+  auto own_step = [&](uint32_t wr, auto&& next) __attribute__((always_inline)) {
+    const u32x4 o = on;
+    uint32_t Y[kBsPlanes];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) Y[p] = ycur[p];
+    transpose8(Y);
+    lds_write(wr, Y);
+    asm volatile("" ::: "memory");                     // the next read stays below the transpose
+    next();
+    NTC_BS_TABLES(Y)
+    chain(o, Y);
+  };
+  auto partner_step = [&](auto&& next) __attribute__((always_inline)) {
+    const u32x4 o = on;
+    uint32_t Y[kBsPlanes];
+    // a real copy (early-clobber asm), so that the allocator does not give ycur the table
+    // registers v2..v9, which are live while the next read lands in ycur
+#pragma unroll
+    for (int p = 0; p < 8; ++p) asm volatile("v_mov_b32 %0, %1" : "=&v"(Y[p]) : "v"(ycur[p]));
+    next();
+    NTC_BS_TABLES(Y)
+    chain(o, Y);
+  };
+
+  // Turns 0 .. nT, where turn nT's own sources are all past k: its own steps transpose the clamped
+  // last source with zero coefficients (the chain returns at once) and exist only so that every
+  // turn has the same steps -- the partner's last sources need no separate tail, and no step's
+  // next read depends on a branch.
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) issue_turn(t);     // turns 0 .. NS-2 (past nT: clamped rows)
+  wait_own(0, 0);
+  lds_read(w * kBsSlot, ycur);
+  on = coef_at(w);
+  // turn 0: own steps only
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    own_step((2 * j + w) * kBsSlot, [&]() __attribute__((always_inline)) {
+      if (j + 1 < J) {
+        wait_own(j + 1, 0);
+        lds_read((2 * j + 2 + w) * kBsSlot, ycur);
+        on = coef_at(2 * j + 2 + w);
+      }
+    });
+  barrier();
+  if (NS - 1 <= nT) issue_turn(NS - 1);
+  wait_own(0, 1);                                      // next: own(1, 0)
+  lds_read(kSet + w * kBsSlot, ycur);
+  on = coef_at(TS + w);
+  // turns 1 .. nT: own(T, j) then partner(T-1, j); S = T % NS at compile time, so the LDS offsets
+  // are immediates
+  auto turn = [&](uint32_t T, auto S) __attribute__((always_inline)) {
+    constexpr uint32_t so = S() * kSet, sn = (S() + 1) % NS * kSet, sp = (S() + NS - 1) % NS * kSet;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      own_step(so + (2 * j + w) * kBsSlot, [&]() __attribute__((always_inline)) {
+        lds_read(sp + (2 * j + 1 - w) * kBsSlot, ycur);    // partner(T-1, j), published last turn
+        on = coef_at((T - 1) * TS + 2 * j + 1 - w);
+      });
+      if (j == J - 1) {
+        barrier();
+        if (T + NS - 1 <= nT) issue_turn(T + NS - 1);
+      }
+      partner_step([&]() __attribute__((always_inline)) {
+        if (j + 1 < J) {                               // own(T, j+1)
+          wait_own(j + 1, T);
+          lds_read(so + (2 * j + 2 + w) * kBsSlot, ycur);
+          on = coef_at(T * TS + 2 * j + 2 + w);
+        } else {                                       // own(T+1, 0) (after turn nT: read, unused)
+          wait_own(0, T + 1);
+          lds_read(sn + w * kBsSlot, ycur);
+          on = coef_at((T + 1) * TS + w);
+        }
+      });
+    }
+  };
+  for (uint32_t T = 1; T <= nT; T += NS) {
+    turn(T, std::integral_constant<uint32_t, 1>());
+    if (T + 1 > nT) break;
+    turn(T + 1, std::integral_constant<uint32_t, 2>());
+    if (T + 2 > nT) break;
+    if constexpr (NS == 4) {
+      turn(T + 2, std::integral_constant<uint32_t, 3>());
+      if (T + 3 > nT) break;
+    }
+    turn(T + NS - 1, std::integral_constant<uint32_t, 0>());
+  }
+
+  const uint32_t row0 = tile * 16u;
+  const uint32_t c0 = col + lane * 16u, c1 = c0 + 1024u;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (static_cast<uint32_t>(j) >= nrows) continue;
+    uint32_t acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = A[j][p];
+    transpose8(acc);
+    uint8_t* dst;
+    if constexpr (DEC) {
+      const uint16_t* outs = a.out_idx + static_cast<size_t>(g) * a.rp + row0;
+      dst = a.out + static_cast<size_t>(g) * a.k * stride + uniform(outs[j]) * stride;
+    } else {
+      dst = a.out + (static_cast<size_t>(g) * a.rows + row0 + j) * stride;
+    }
+    if (v0) *reinterpret_cast<uint4*>(dst + c0) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+    if (v1) *reinterpret_cast<uint4*>(dst + c1) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+// One 2-wave workgroup per (generation, pair of 16-row tiles, 2 KiB column span), blocks renumbered
+// per XCD as in gf_mac_bs.  A pair whose second tile has no rows (a decode generation with m <= 16,
+// the last tile of an odd tile count) runs gf_mac_bs's single-wave tile instead.
+template <int J, int NS, bool DEC, bool FULL>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(3))) void gf_mac_bsp(MacArgs a)
+{
+  static_assert(NS * 2 * J >= kBsRing, "the single-tile path uses a kBsRing-slot ring");
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[NS * 2 * J * kBsSlot];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = uniform(threadIdx.x >> 6);
+  const uint32_t nb = gridDim.x;                       // a multiple of 8 (launch_mac)
+  uint32_t task = uniform((blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3));
+  const uint32_t npair = (a.nrowchunks + 1) / 2;
+  uint32_t cc, tp;
+  if (a.tile_fast) {
+    tp = task % npair;
+    task /= npair;
+    cc = task % a.ncolchunks;
+    task /= a.ncolchunks;
+  } else {
+    cc = task % a.ncolchunks;
+    task /= a.ncolchunks;
+    tp = task % npair;
+    task /= npair;
+  }
+  const uint32_t g = task;
+  if (g >= a.G) return;
+  const uint32_t total = DEC ? const_load_u16(a.rows_per_gen + g) : a.rows;
+  const uint32_t row0 = tp * 32u;
+  if (row0 >= total) return;
+  const uint32_t ring = lds_addr(s_ring);
+  if (total - row0 <= 16u) {                           // one tile: wave 0 alone
+    if (w) return;
+    bs_tile<16, DEC, FULL>(a, g, 2 * tp, total - row0, cc, lane, ring);
+    return;
+  }
+  const uint32_t nrows = w ? min(16u, total - row0 - 16u) : 16u;
+  if (w == 0) bs_pair<J, NS, DEC, FULL, 0>(a, g, 2 * tp, nrows, cc, lane, ring);
+  else bs_pair<J, NS, DEC, FULL, 1>(a, g, 2 * tp + 1, nrows, cc, lane, ring);
+}
+
 // ---- grouped bit-sliced MAC: NT row tiles of one (generation, span) share the source fill ----
 // The per-source fill -- the 8x8 bit transpose and the 22 plane-table XORs, 70+ VALU -- depends
 // only on the source, not on the row tile, yet every 16-row tile of a generation repeated it.
@@ -2645,7 +2922,8 @@ bool use_bitslice(const ntc_gf256_engine* e, uint32_t stride)
 {
   if (stride % 16 != 0) return false;
   if (e->mac_kind != NTC_GF256_MAC_AUTO)
-    return e->mac_kind == NTC_GF256_MAC_BITSLICE || e->mac_kind == NTC_GF256_MAC_BITSLICE_GROUPED;
+    return e->mac_kind == NTC_GF256_MAC_BITSLICE || e->mac_kind == NTC_GF256_MAC_BITSLICE_GROUPED ||
+           e->mac_kind == NTC_GF256_MAC_BITSLICE_PAIRED;
   const uint32_t pieces = stride / 16, spans = (stride + 2047) / 2048;   // 16-B pieces per span: 128
   return pieces * 100 >= spans * 128 * 33;
 }
@@ -2659,6 +2937,19 @@ mac_fn pick_bs(bool dec, uint32_t rowtile, bool full, bool pair)
                : (full ? gf_mac_bs<16, false, true> : gf_mac_bs<16, false, false>);
   return dec ? (full ? gf_mac_bs<8, true, true> : gf_mac_bs<8, true, false>)
              : (full ? gf_mac_bs<8, false, true> : gf_mac_bs<8, false, false>);
+}
+
+template <int J, int NS>
+mac_fn pick_bsp_(bool dec, bool full)
+{
+  return dec ? (full ? gf_mac_bsp<J, NS, true, true> : gf_mac_bsp<J, NS, true, false>)
+             : (full ? gf_mac_bsp<J, NS, false, true> : gf_mac_bsp<J, NS, false, false>);
+}
+
+mac_fn pick_bsp(bool dec, bool full, int j, int ns)
+{
+  if (j == 2) return ns == 4 ? pick_bsp_<2, 4>(dec, full) : pick_bsp_<2, 3>(dec, full);
+  return ns == 4 ? pick_bsp_<1, 4>(dec, full) : pick_bsp_<1, 3>(dec, full);
 }
 
 mac_fn pick_bsg(bool dec, bool full)
@@ -2715,6 +3006,7 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   uint32_t rowtile, span, wpb;
   uint64_t blk_align = 1;
   uint32_t group = 1;                           // 16-row tiles per workgroup sharing the fill
+  bool paired = false;                          // gf_mac_bsp: tile pairs sharing the transpose
   if (a.pair || use_bitslice(e, a.stride)) {
     // 16-row tiles (3 waves per SIMD) once a tile has more than 8 rows to fill, else 8-row
     // tiles (4 waves per SIMD)
@@ -2727,10 +3019,13 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       group = 2;                                // gf_mac_bsg: tile pairs share the source fill
       fn = pick_bsg(dec, a.stride % 2048 == 0);
     }
+    if (!a.pair && rowtile == 16 && e->mac_kind == NTC_GF256_MAC_BITSLICE_PAIRED && a.rows > 16)
+      paired = true;                            // gf_mac_bsp, unless sliced or split below
     // a tall encode / combine over whole spans: slice the sources once (bs_preslice) instead of
     // once per row tile
     if (!dec && !a.pair && group == 1 && a.stride % 2048 == 0 &&
         (e->slice_force >= 0 ? e->slice_force != 0 : a.rows >= kSliceRows)) {
+      paired = false;
       const uint64_t n = static_cast<uint64_t>(a.G) * a.k * a.stride;
       // as for the split-k parts: a stream being captured must not allocate; and the copy is an
       // optimisation, so without room for it (hipMalloc fails) the MAC slices in registers
@@ -2738,10 +3033,11 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
       const bool capturing = hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
       if (n > e->slice_cap && !capturing) {
         void* p = nullptr;
-        if (hipMalloc(&p, n) == hipSuccess) {
+        const size_t na = grow_to(e, n, e->slice_cap);
+        if (hipMalloc(&p, na) == hipSuccess) {
           drop_buf(e, e->slice);
           e->slice = p;
-          e->slice_cap = n;
+          e->slice_cap = na;
         } else {
           (void)hipGetLastError();             // clear it: the call proceeds unsliced
         }
@@ -2828,10 +3124,11 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
   if (a.ksplit > 1 && (a.ksplit - 1) * a.kout_step > e->kout_cap) {
     // the split is an optimisation: without room for the parts the MAC runs unsplit
     void* p = nullptr;
-    if (hipMalloc(&p, (a.ksplit - 1) * a.kout_step) == hipSuccess) {
+    const size_t na = grow_to(e, (a.ksplit - 1) * a.kout_step, e->kout_cap);
+    if (hipMalloc(&p, na) == hipSuccess) {
       drop_buf(e, e->kout);
       e->kout = p;
-      e->kout_cap = (a.ksplit - 1) * a.kout_step;
+      e->kout_cap = na;
     } else {
       (void)hipGetLastError();
       a.ksplit = 1;
@@ -2846,12 +3143,19 @@ int launch_mac(ntc_gf256_engine* e, bool dec, MacArgs& a, hipStream_t st, const 
     tasks = tasks / a.nrowchunks * ((a.nrowchunks + group - 1) / group);
     wpb = 4 / group;
   }
+  uint32_t threads = group > 1 ? 256 : 64 * wpb;
+  if (paired && a.ksplit == 1) {                // one 2-wave workgroup per tile pair
+    fn = pick_bsp(dec, a.stride % 2048 == 0, e->pair_j, e->pair_sets);
+    tasks = tasks / a.nrowchunks * ((a.nrowchunks + 1) / 2);
+    wpb = 1;
+    threads = 128;
+  }
   const uint64_t blocks = ((tasks + wpb - 1) / wpb + blk_align - 1) / blk_align * blk_align;
   if (blocks > 0x7FFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
   if (e->timing) (void)hipEventRecord(e->mac_ev[dec][0], st);
   {
     KernelTimer kt(e, dec ? NTC_GF256_K_DECODE_MAC : NTC_GF256_K_ENCODE_MAC, st, true);
-    hipExtLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(group > 1 ? 256 : 64 * wpb), 0,
+    hipExtLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(threads), 0,
                           st, kt.start(), kt.stop(), 0, a);
   }
   int rc = hip_check(hipGetLastError(), what);
@@ -2887,15 +3191,23 @@ void drop_buf(ntc_gf256_engine* e, void* p)
   else (void)hipFree(p);
 }
 
+size_t grow_to(const ntc_gf256_engine* e, size_t need, size_t cap)
+{
+  // after a capture every outgrown buffer is retired, not freed: grow geometrically so that a
+  // run of slowly rising shapes retires few of them
+  return e->captured_any ? std::max(need, 2 * cap) : need;
+}
+
 int ensure_buf(ntc_gf256_engine* e, void** p, size_t* cap, size_t need, const char* what)
 {
   if (need <= *cap) return NTC_GPU_OK;
+  const size_t n = grow_to(e, need, *cap);
   drop_buf(e, *p);
   *p = nullptr;
   *cap = 0;
-  int rc = hip_check(hipMalloc(p, need), what);
+  int rc = hip_check(hipMalloc(p, n), what);
   if (rc) return rc;
-  *cap = need;
+  *cap = n;
   return NTC_GPU_OK;
 }
 
@@ -2906,7 +3218,7 @@ namespace {
 int ensure_plan(ntc_gf256_engine* e, uint32_t G, uint32_t k, uint32_t rp)
 {
   if (G <= e->plan_cap_G && k <= e->plan_cap_k && rp <= e->plan_cap_rp) return NTC_GPU_OK;
-  const size_t nG = G > e->plan_cap_G ? G : e->plan_cap_G;
+  const size_t nG = G > e->plan_cap_G ? grow_to(e, G, e->plan_cap_G) : e->plan_cap_G;
   const size_t nk = k > e->plan_cap_k ? k : e->plan_cap_k;
   const size_t nrp = rp > e->plan_cap_rp ? rp : e->plan_cap_rp;
   (void)hipSetDevice(e->device);
@@ -2981,6 +3293,15 @@ int ntc_gf256_engine_create(int device, ntc_gf256_engine** out)
     if (!std::strcmp(m, "perm")) e->mac_kind = NTC_GF256_MAC_PERM;
     else if (!std::strcmp(m, "bitslice")) e->mac_kind = NTC_GF256_MAC_BITSLICE;
     else if (!std::strcmp(m, "grouped")) e->mac_kind = NTC_GF256_MAC_BITSLICE_GROUPED;
+    else if (!std::strcmp(m, "paired")) e->mac_kind = NTC_GF256_MAC_BITSLICE_PAIRED;
+  }
+  if (const char* t = std::getenv("NTC_GF256_PAIRJ")) {
+    if (!std::strcmp(t, "1")) e->pair_j = 1;
+    else if (!std::strcmp(t, "2")) e->pair_j = 2;
+  }
+  if (const char* t = std::getenv("NTC_GF256_PAIRSETS")) {
+    if (!std::strcmp(t, "3")) e->pair_sets = 3;
+    else if (!std::strcmp(t, "4")) e->pair_sets = 4;
   }
   if (const char* t = std::getenv("NTC_GF256_KSPLIT")) {
     const int v = std::atoi(t);
@@ -3053,8 +3374,17 @@ int ntc_gf256_mac_time(ntc_gf256_engine* e, int dec, float* ms)
 int ntc_gf256_set_mac_kind(ntc_gf256_engine* e, int kind)
 {
   if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
-  if (kind < NTC_GF256_MAC_AUTO || kind > NTC_GF256_MAC_BITSLICE_GROUPED) return fail(NTC_GPU_EINVAL, "unknown MAC kind");
+  if (kind < NTC_GF256_MAC_AUTO || kind > NTC_GF256_MAC_BITSLICE_PAIRED) return fail(NTC_GPU_EINVAL, "unknown MAC kind");
   e->mac_kind = kind;
+  return NTC_GPU_OK;
+}
+
+int ntc_gf256_release_retired(ntc_gf256_engine* e)
+{
+  if (!e) return fail(NTC_GPU_EINVAL, "engine is NULL");
+  (void)hipSetDevice(e->device);
+  for (void* b : e->retired) (void)hipFree(b);
+  e->retired.clear();
   return NTC_GPU_OK;
 }
 

@@ -95,7 +95,7 @@ class Engine:
     def handle(self):
         return self._h
 
-    MAC_KINDS = {"auto": 0, "perm": 1, "bitslice": 2, "grouped": 3}
+    MAC_KINDS = {"auto": 0, "perm": 1, "bitslice": 2, "grouped": 3, "paired": 4}
 
     def set_mac_kind(self, kind: str = "auto"):
         """Select the region-MAC formulation (ntc_gf256_set_mac_kind); results are identical."""

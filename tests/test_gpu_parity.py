@@ -50,7 +50,7 @@ def gpu_decode(d, lost, llen, smask, rep, rsz, rmask, sid=None, rid=None):
     return host(s_t), host(l_t, np.uint16), status_to_numpy(st)
 
 
-@pytest.fixture(params=["auto", "perm", "bitslice", "grouped"])
+@pytest.fixture(params=["auto", "perm", "bitslice", "grouped", "paired"])
 def mac(request, gpu):
     """Run a parity test under each region-MAC formulation (ntc_gf256_set_mac_kind)."""
     from netcode_amd.engine import Engine

@@ -73,6 +73,14 @@ def test_tall_combine_sliced_under_graph_capture(gpu, oracle):
         torch.cuda.synchronize(gpu)
         assert not big_o.any()
         assert (replay(*sliced) == ref).all()
+        # once the graphs are gone the retired buffers can be freed; the engine keeps working
+        del sliced
+        torch.cuda.synchronize(gpu)
+        _native.check(L.ntc_gf256_release_retired(h), "release retired")
+        out.fill_(0xA5)
+        combine(out, torch.cuda.current_stream(gpu).cuda_stream)
+        torch.cuda.synchronize(gpu)
+        assert (out.cpu().numpy() == ref).all()
     finally:
         torch.cuda.synchronize(gpu)
         L.ntc_gf256_engine_destroy(h)

@@ -69,6 +69,7 @@ def parse():
     p.add_argument("--G", type=int, default=0, help="generations per GPU (default per config)")
     p.add_argument("--S", type=int, default=0, help="symbol bytes (exploration; default per config)")
     p.add_argument("--stride", type=int, default=0, help="row pitch in HBM (multiple of 16, >= S; default per config)")
+    p.add_argument("--r", type=int, default=0, help="repairs per generation (exploration; m capped at r)")
     p.add_argument("--mixed", action="store_true", help="m ~ U[0, r] instead of m = r")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-rate", action="store_true")
@@ -328,6 +329,14 @@ def host_rate(w, reps=3):
     return rate_packed, rate_pipe, rate_serial, packed_ok
 
 
+# The bit-sliced chain alone (the product's shared-table chain, no fill, no memory stream) on
+# MI355X: 51.5 cycles per 2048-byte-MAC wave-row per SIMD = 98 T byte-MAC/s
+# (profiles/r03/microbench_chain_README.md, tools/gen_microbench_chain.py).
+CHAIN_PEAK_TBMAC = 98.0
+CHAIN_PEAK_SOURCE = ("chain microbenchmark, product chain R8 W4: 51.5 cycles/row/SIMD = 98 T "
+                     "byte-MAC/s (profiles/r03/microbench_chain_README.md)")
+
+
 def cpu_info():
     """(model name, nproc of this machine, CPUs this process may run on)."""
     model = "unknown"
@@ -365,6 +374,14 @@ def cpu_quota():
         per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
         return round(q / per, 2)
     return None
+
+
+def effective_cpus():
+    """CPUs this process can actually use: the affinity mask, capped by the cgroup CPU quota
+    (a gpurun box lists every CPU of the machine in the mask but grants 16 of them)."""
+    _, _, usable = cpu_info()
+    q = cpu_quota()
+    return max(1, min(usable, int(q))) if q else usable
 
 
 def cpu_baseline_run(k, r, S, stride, m, threads, budget_s):
@@ -444,7 +461,9 @@ def cpu_baseline(k, r, S, stride, m, threads, budget_s=12.0):
                             "encode_s": round(e1, 3), "decode_s": round(d1, 3)},
             "gfni_upper_bound": gfni,
             "cpu_model": model, "nproc": nproc, "usable_cpus": usable,
-            "cgroup_cpu_quota": cpu_quota()}
+            "cgroup_cpu_quota": cpu_quota(), "effective_cpus": effective_cpus(),
+            "cores_note": "cores = the threads of the all-core leg = the effective CPU count "
+                          "(affinity mask capped by the cgroup quota)"}
 
 
 def _pp_encode(mk_enc, a, data, batch=None):
@@ -817,6 +836,8 @@ def main():
         assert a.stride >= S and a.stride % 16 == 0, "--stride: a multiple of 16, at least S"
         stride = a.stride
     G = a.G or Gdef
+    if a.r:                              # exploration: fewer / more repairs (m capped at r)
+        r, m = a.r, min(m, a.r)
 
     if world == 1:
         import __graft_entry__
@@ -973,6 +994,20 @@ def main():
             "byte_mac_rate_T_per_s": round(macs / (t_dom * 1e-3) / 1e12, 2),
             "valu_profile": valu, "valu_profile_source": vsrc,
             "hbm_copy_probe_GBps": probe if probe is not None else hbm_copy_probe(dev)}
+    if dense:
+        # config 5 is compute-class: each source feeds 1024 rows, so its MACs are bound by the
+        # bit-sliced chain, not HBM (0.13 GB per 0.78-ms launch).  Primary roofline: the byte-MAC
+        # rate against the chain's measured ceiling; the HBM fraction stays as a secondary field.
+        bm = macs / (t_dom * 1e-3) / 1e12
+        hbm = {k_: roof.pop(k_) for k_ in ("achieved", "peak", "unit", "frac")}
+        roof.pop("bound")
+        roof = {"bound": "valu", "achieved": round(bm, 2), "peak": CHAIN_PEAK_TBMAC,
+                "unit": "T byte-MAC/s", "frac": round(bm / CHAIN_PEAK_TBMAC, 4),
+                "peak_source": CHAIN_PEAK_SOURCE,
+                "valu_issue_frac": (valu or {}).get("valu_issue_frac"),
+                "hbm_secondary": {**hbm, "note": "algorithmic bytes (k + n)*S per launch over its "
+                                                 "duration, against the 8 TB/s HBM peak"},
+                **roof}
 
     line = {"metric": metric_name(a.config, k, r, S),
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": n_gpus, "ranks": world,
@@ -1040,8 +1075,7 @@ def main():
             smp["rep_pkts"] = rpk.view(G, r, -1)[gi].numpy()
             smp["rep_pkt_len"] = rpl.view(G, r)[gi].numpy()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        _, _, usable = cpu_info()
-        thr = a.cpu_threads or usable          # every CPU this process may run on
+        thr = a.cpu_threads or effective_cpus()   # the CPUs this process actually gets
         line["cpu_baseline"] = (cpu_baseline_dense(w) if dense
                                 else cpu_baseline(k, r, S, stride, m, thr))
         if smp is not None:

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +31,7 @@
 #include "netcode/c/encoder.h"
 #include "netcode/c/ext.h"
 #include "netcode/gpu.h"
+#include "gf256_field.hh"
 
 namespace ntcx {
 
@@ -50,12 +52,17 @@ struct Align16 {
   using value_type = T;
   Align16() = default;
   template <typename U> Align16(const Align16<U>&) {}
+  // malloc already returns 16-byte aligned blocks on x86-64 (alignof(max_align_t) = 16 there;
+  // this host code is built for x86-64 only): the aligned operator new would take glibc's
+  // memalign path, which bypasses the per-thread cache -- every payload, packet and result buffer
+  // of the batching adaptor is one of these
   T* allocate(size_t n)
   {
-    void* p = ::operator new(n * sizeof(T) + 0, std::align_val_t(16));
+    void* p = std::malloc(n * sizeof(T) ? n * sizeof(T) : 1);
+    if (!p) throw std::bad_alloc();
     return static_cast<T*>(p);
   }
-  void deallocate(T* p, size_t) { ::operator delete(p, std::align_val_t(16)); }
+  void deallocate(T* p, size_t) { std::free(p); }
   // resize(n) default-initialises (no zeroing), like the reference's byte_buffer (buffer.hh:66-73);
   // resize(n, 0) and assign(n, 0) still zero-fill
   template <typename U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
@@ -317,7 +324,9 @@ class Device {
         stack.pop_back();
       }
     }
-    std::stable_sort(todo.begin(), todo.end(), [](const Node* a, const Node* b) { return a->level < b->level; });
+    auto by_level = [](const Node* a, const Node* b) { return a->level < b->level; };
+    if (!std::is_sorted(todo.begin(), todo.end(), by_level))   // (often one level: encoder repairs)
+      std::stable_sort(todo.begin(), todo.end(), by_level);
     std::vector<Node*> t8, tw;
     for (Node* n : todo) (n->w == 8 ? t8 : tw).push_back(n);
     NTC_PROF_ADD(walk, t_walk);
@@ -759,13 +768,18 @@ struct Field {
     if (w != 4 && w != 8 && w != 16 && w != 32)
       throw std::invalid_argument("galois field size must be 4, 8, 16 or 32");
   }
+  // w = 8 inline (the engine library's compile-time tables): these run per window source of
+  // every repair, so no call through the shared library's PLT
   uint32_t coef(uint32_t rid, uint32_t sid) const
   {
-    return w == 8 ? ntc_gf256_coefficient(rid, sid) : ntc_gf_coefficient(w, rid, sid);
+    return w == 8 ? ntcgpu::coefficient(rid, sid) : ntc_gf_coefficient(w, rid, sid);
   }
   uint16_t msize(uint16_t s, uint32_t c) const
   {
-    return w == 8 ? ntc_gf256_multiply_size(s, c) : ntc_gf_multiply_size(w, s, c);
+    if (w != 8) return ntc_gf_multiply_size(w, s, c);
+    const uint8_t cc = static_cast<uint8_t>(c);       // galois_field.hh:108-115 (bytewise)
+    return static_cast<uint16_t>(ntcgpu::field_mul(cc, static_cast<uint8_t>(s & 0xFF)) |
+                                 (ntcgpu::field_mul(cc, static_cast<uint8_t>(s >> 8)) << 8));
   }
   uint32_t mul(uint32_t a, uint32_t b) const
   {
@@ -835,8 +849,14 @@ struct Reader {
   std::vector<uint32_t> ids()                   // packetizer.hh:312-352 (sorted, unique)
   {
     std::vector<uint32_t> v;
+    ids_into(v);
+    return v;
+  }
+  void ids_into(std::vector<uint32_t>& v)        // the same into v (cleared; capacity reused)
+  {
+    v.clear();
     const uint16_t ne = u16();
-    if (ne == 0) return v;
+    if (ne == 0) return;
     uint32_t acc = u32();
     v.reserve(32);
     v.push_back(acc);
@@ -854,7 +874,6 @@ struct Reader {
       std::sort(v.begin(), v.end());
       v.erase(std::unique(v.begin(), v.end()), v.end());
     }
-    return v;
   }
 };
 
@@ -931,9 +950,10 @@ class Encoder {
       const bool now = emit_now();
       if (now) out_.buf = nullptr;
       else begin(p, 7 + s.sym->size);
-      out_.u8(2);                                  // packetizer.hh:165-183
-      out_.u32(s.id);
-      out_.u16(s.sym->size);
+      // packetizer.hh:165-183: the 7-byte header in one piece, then the payload
+      const uint8_t hdr[7] = {2, uint8_t(s.id >> 24), uint8_t(s.id >> 16), uint8_t(s.id >> 8), uint8_t(s.id),
+                              uint8_t(s.sym->size >> 8), uint8_t(s.sym->size)};
+      out_.raw(hdr, 7);
       out_.raw(s.sym->data(), s.sym->size);
       out_.end();
       if (!now) finish(std::move(p));
@@ -955,6 +975,12 @@ class Encoder {
     Expr terms;
     if (batch_) terms.reserve(window_.size());
     else { in_.clear(); lens_.clear(); cs_.clear(); }
+    // encoded size = XOR of msize(len_i, c_i) (detail/encoder.cc:38, 61-62); with equal lengths
+    // (the usual case) that is msize(len, XOR of c_i) -- the product distributes over XOR -- so
+    // one product per repair instead of one per source (w = 8 and w = 4: bytewise size coding)
+    const uint16_t sz0 = window_.front().sym->size;
+    bool same = f_.w <= 8;
+    uint32_t cx = 0;
     for (const Src& s : window_) {
       const uint32_t c = f_.coef(cur_rid_, s.id);
       const uint16_t sz = s.sym->size;
@@ -967,8 +993,16 @@ class Encoder {
       }
       ids_.push_back(s.id);
       symsz = std::max<uint16_t>(symsz, sz);
-      esz = static_cast<uint16_t>(f_.msize(sz, c) ^ esz);
+      if (same && sz == sz0) cx ^= c;
+      else {
+        if (same) {                                // first unequal length: the per-source form
+          same = false;
+          esz = f_.msize(sz0, cx);
+        }
+        esz = static_cast<uint16_t>(f_.msize(sz, c) ^ esz);
+      }
     }
+    if (same) esz = f_.msize(sz0, cx);
     bytes sym;
     if (!batch_) {
       sym.resize(symsz);
@@ -1236,10 +1270,10 @@ class Decoder {
       const uint32_t id = rd.u32();
       const uint16_t symsz = rd.u16();
       const uint8_t* sym = rd.skip(symsz);
-      std::vector<uint32_t> ids = rd.ids();
+      rd.ids_into(ids_);                           // (scratch: no allocation per repair)
       const uint16_t esz = rd.u16();
       const size_t consumed = n - rd.left;
-      if (!ids.empty()) on_repair(id, std::move(ids), esz, sym, symsz, own);
+      if (!ids_.empty()) on_repair(id, ids_, esz, sym, symsz, own);
       return consumed;
     }
     if (ty == 2) {
@@ -1391,11 +1425,18 @@ class Decoder {
     if (known.empty()) return;
     if (batch_) {                // one term per source payload, whatever produced it
       r.red.reserve(r.red.size() + known.size());
+      // encoded-size update: XOR of msize(size_i, c_i); equal sizes (the usual case) make that
+      // one product of the XORed coefficients (galois_field.hh:96-120 is linear in c)
+      const uint16_t sz0 = known.front()->size;
+      bool same = f_.w <= 8;
+      uint32_t cx = 0;
       for (const Src* s : known) {
         const uint32_t c = f_.coef(r.id, s->id);
-        r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
+        if (same && s->size == sz0) cx ^= c;
+        else r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
         r.red.push_back(Term{s->node, c, std::min<uint16_t>(s->size, r.symsz)});
       }
+      if (cx) r.esz = static_cast<uint16_t>(f_.msize(sz0, cx) ^ r.esz);
       return;
     }
     std::vector<const uint8_t*> in{r.sym.data()};
@@ -1445,34 +1486,41 @@ class Decoder {
   }
 
   // detail/decoder.cc:54-152
-  void on_repair(uint32_t id, std::vector<uint32_t>&& ids, uint16_t esz, const uint8_t* sym, uint16_t symsz,
+  // ids: the repair's source ids (sorted; a scratch vector of the caller, read only)
+  void on_repair(uint32_t id, const std::vector<uint32_t>& ids, uint16_t esz, const uint8_t* sym, uint16_t symsz,
                  bytes* own = nullptr)
   {
     if (has_last_ && ids.back() < last_id_) return;
     if (repairs_.count(id)) return;
     drop_outdated(ids.front());
-    bool useless = true;
-    for (uint32_t sid : ids) if (!sources_.count(sid)) { useless = false; break; }
-    if (useless) { ++nb_useless_; return; }
-    Rep& r = repairs_.emplace(id, Rep{id, std::move(ids), esz, bytes(), symsz, {}}).first->second;
-    if (batch_)
+    // known / missing split first (the reference walks the ids in reverse, decoder.cc:102-130;
+    // the order only matters for XOR, which is order-free), so the stored repair is built once
+    // with its remaining ids -- no id vector per repair beyond the one it keeps
+    known_.clear();
+    size_t nrem = 0;
+    for (uint32_t sid : ids) {
+      auto s = sources_.find(sid);
+      if (s != sources_.end()) known_.push_back(&s->second);
+      else ++nrem;
+    }
+    if (nrem == 0) { ++nb_useless_; return; }
+    std::vector<uint32_t> remaining;
+    remaining.reserve(nrem);
+    for (uint32_t sid : ids)
+      if (!sources_.count(sid)) {
+        missing_[sid].insert(id);
+        remaining.push_back(sid);
+      }
+    Rep& r = repairs_.emplace(id, Rep{id, std::move(remaining), esz, bytes(), symsz, {}}).first->second;
+    if (batch_) {
+      r.red.reserve(1 + known_.size());
       r.red.push_back(Term{own ? adopt_node(std::move(*own), sym - own->data(), symsz) : base_node(sym, symsz),
                            1, symsz});
-    else r.sym.assign(sym, sym + symsz);
-    if (!batch_ && r.sym.empty()) r.sym.resize(1, 0);
-    std::vector<const Src*> known;
-    std::vector<uint32_t> remaining;
-    for (auto it = r.ids.rbegin(); it != r.ids.rend(); ++it) {
-      auto s = sources_.find(*it);
-      if (s != sources_.end()) known.push_back(&s->second);
-      else {
-        missing_[*it].insert(id);
-        remaining.push_back(*it);
-      }
+    } else {
+      r.sym.assign(sym, sym + symsz);
     }
-    remove_sources_data(r, known);
-    std::reverse(remaining.begin(), remaining.end());
-    r.ids = std::move(remaining);
+    if (!batch_ && r.sym.empty()) r.sym.resize(1, 0);
+    remove_sources_data(r, known_);
     if (r.ids.size() == 1) {
       Src s = create_source_from_repair(r);
       missing_.erase(s.id);
@@ -1676,6 +1724,8 @@ class Decoder {
   bool in_order_;
   Writer out_;
   ntc_data_handler dh_;
+  std::vector<uint32_t> ids_;          // scratch of add_packet / on_repair
+  std::vector<const Src*> known_;
   uint32_t first_missing_ = 0;
   OrderedIds ordered_;
   FlatMap<uint32_t, Src> sources_;

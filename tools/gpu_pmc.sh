@@ -10,7 +10,6 @@ for C in $CFGS; do
   timeout -k 10 400 python $R/bench.py --config $C $EXTRA > $OUT/bench_$C.log 2>&1 || { tail -20 $OUT/bench_$C.log; exit 1; }
   echo "$C: $(grep '^{' $OUT/bench_$C.log | cut -c1-160)"
   [ -n "$EXTRA" ] && continue
-  [ "$C" = "k1024dense" ] && continue
   B="$R/bench.py --config $C --steps 2 --warmup 1 --no-cpu-baseline --no-host-rate"
   (cd /tmp
    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/$C/fetch -o run -- python3 $B > $OUT/$C.fetch.log 2>&1 &&

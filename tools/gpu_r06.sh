@@ -78,6 +78,14 @@ for s in "${S[@]}"; do
         NTC_GF256_LIB=$LIB NTC_GF256_MAC=$K NTC_GF256_PAIRJ=$J NTC_GF256_PAIRSETS=$NS run pab_$K$J$NS$(basename "${LIB:-x}" .so)_$rep 300 python bench.py --no-cpu-baseline --no-host-rate $BARGS
       done; done
       for f in $OUT/pab_*.log; do python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); print('$f', d['value'], d['ms_per_step'], d['kernels_ms'])"; done ;;
+    c4tile)    # config-4 read traffic with one row tile per generation (r = 16) against two (r = 32):
+               # if the two tiles refetch sources from HBM, the excess over the rows' bytes vanishes at r = 16
+      for R in 16 32; do
+        B="$PWD/bench.py --config k128r32s1500 --r $R --steps 2 --warmup 1 --no-cpu-baseline --no-host-rate"
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $OLDPWD/$OUT/c4tile_$R/fetch -o run -- python3 $B > $OLDPWD/$OUT/c4tile_$R.fetch.log 2>&1) || { echo "fetch pass r=$R failed"; exit 1; }
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $OLDPWD/$OUT/c4tile_$R/write -o run -- python3 $B > $OLDPWD/$OUT/c4tile_$R.write.log 2>&1) || { echo "write pass r=$R failed"; exit 1; }
+        echo "c4tile r=$R done"
+      done ;;
     parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_random_shapes.py -x -q -m gpu --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

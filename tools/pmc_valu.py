@@ -21,7 +21,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"encode_mac": (r"gf_mac_bs<\d+, false", r"gf_mac<\d, false"),
            "decode_mac": (r"gf_mac_bs<\d+, true", r"gf_mac<\d, true")}
 CONFIGS = {"k128r32s4096": (128, 32, 4096, 4096, 32),   # k, r, S, G, m
-           "k32r8s1024": (32, 8, 1024, 4096, 8), "k128r32s1500": (128, 32, 1500, 8192, 32)}
+           "k32r8s1024": (32, 8, 1024, 4096, 8), "k128r32s1500": (128, 32, 1500, 8192, 32),
+           "k1024dense": (1024, 1024, 65536, 1, 1024)}
+# config 5: the dense encode and the dense decode (the inverse applied as a combine) are the same
+# kernel -- the sliced-source encode MAC -- so one counter entry serves both keys
+DENSE_KERNELS = {"encode_mac": (r"gf_mac_bs<16, false, true, false, true>",),
+                 "decode_mac": (r"gf_mac_bs<16, false, true, false, true>",)}
 HOW = "rocprofv3 --pmc, 2 SQ passes of bench.py --steps 2 --warmup 1 (tools/gpu_pmc.sh)"
 
 
@@ -57,7 +62,7 @@ def main():
     out_p = os.path.join(ROOT, "profiles", "pmc_valu.json")
     out = json.load(open(out_p)) if os.path.exists(out_p) else {}
     ent = {}
-    for key, names in KERNELS.items():
+    for key, names in (DENSE_KERNELS if cfg == "k1024dense" else KERNELS).items():
         cs = next((v for n, v in table.items() if any(re.search(x, n) for x in names)), None)
         if cs is None:
             continue

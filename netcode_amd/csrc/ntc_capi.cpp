@@ -46,23 +46,122 @@ struct device_error : std::runtime_error {
   explicit device_error(const std::string& m) : std::runtime_error(m) {}
 };
 
+// ------------------------------------------------------------- pinned payload blocks ----
+// Every byte buffer of the adaptor (data objects, packets, payload nodes: `bytes` below) is a
+// block of pinned host memory when a HIP device is present: the GPU then reads a new payload
+// straight from the buffer the application filled (an upload job of the flush's first launch, one
+// PCIe read) and writes each result straight into the buffer its node keeps -- no staging copy
+// in, no copy out (DESIGN.md §3 batching; CPU access to these blocks runs at the speed of
+// malloc'd memory, tools/pinned_probe.hip).  Size classes: n rounded up to 1/8 of its power of
+// two (64 B .. 128 KiB), carved from 4 MiB hipHostMalloc slabs that are never returned (the
+// adaptor's peak payload memory stays reserved for the process); larger buffers, and every buffer
+// without a device (or in the host-stub build), are malloc'd.  A spin lock guards the free lists.
+class BlockPool {
+ public:
+  static BlockPool& get()
+  {
+    static BlockPool* p = new BlockPool;       // never destroyed (blocks outlive static teardown)
+    return *p;
+  }
+  static constexpr size_t kMaxBlock = size_t(128) << 10;
+  bool pinned() const { return pinned_; }
+  // whether a buffer of capacity n came from the pinned pool
+  bool pooled(size_t n) const { return pinned_ && n <= kMaxBlock; }
+  void* alloc(size_t n)
+  {
+    if (!pooled(n)) {
+      void* p = std::malloc(n ? n : 1);      // 16-byte aligned on x86-64 (alignof(max_align_t))
+      if (!p) throw std::bad_alloc();
+      return p;
+    }
+    const int c = cls(n);
+    lock();
+    void* p = free_[c];
+    if (p) free_[c] = *static_cast<void**>(p);
+    else p = carve(csize(c));
+    unlock();
+    if (!p) throw std::bad_alloc();
+    return p;
+  }
+  void release(void* p, size_t n)
+  {
+    if (!pooled(n)) {
+      std::free(p);
+      return;
+    }
+    const int c = cls(n);
+    lock();
+    *static_cast<void**>(p) = free_[c];
+    free_[c] = p;
+    unlock();
+  }
+
+ private:
+  static constexpr size_t kSlab = size_t(4) << 20;
+  static constexpr int kClasses = 12 * 8;      // 2^6 .. 2^17, 8 steps each
+  BlockPool()
+  {
+#ifndef NTC_CAPI_HOST_STUB
+    int n = 0;
+    void* p = nullptr;
+    if (std::getenv("NTC_BATCH_UNPINNED") == nullptr && hipGetDeviceCount(&n) == hipSuccess && n > 0 &&
+        hipHostMalloc(&p, kSlab, hipHostMallocDefault) == hipSuccess) {
+      slab_ = static_cast<uint8_t*>(p);
+      left_ = kSlab;
+      pinned_ = true;
+    } else {
+      (void)hipGetLastError();
+    }
+#endif
+  }
+  // class of n: its power of two 2^k (k >= 6) in steps of 2^(k-3)
+  static int cls(size_t n)
+  {
+    if (n <= 64) return 0;
+    const int k = 64 - __builtin_clzll(n - 1);                // 2^(k-1) < n <= 2^k
+    const size_t g = size_t(1) << (k - 3);
+    const int j = static_cast<int>((n + g - 1) / g) - 4;       // 5..8 eighths -> 1..4 ... 
+    return (k - 6) * 8 + (j < 0 ? 0 : j);
+  }
+  static size_t csize(int c)
+  {
+    const int k = c / 8 + 6, j = c % 8;
+    return c == 0 ? 64 : (size_t(1) << (k - 3)) * static_cast<size_t>(j + 4);
+  }
+  void* carve(size_t b)                        // under the lock
+  {
+#ifndef NTC_CAPI_HOST_STUB
+    if (left_ < b) {                           // a new slab (the old one's tail, < 128 KiB, stays unused)
+      void* p = nullptr;
+      if (hipHostMalloc(&p, kSlab, hipHostMallocDefault) != hipSuccess) return nullptr;
+      slab_ = static_cast<uint8_t*>(p);
+      left_ = kSlab;
+    }
+#endif
+    void* r = slab_;
+    slab_ += b;
+    left_ -= b;
+    return r;
+  }
+  void lock() { while (lk_.test_and_set(std::memory_order_acquire)) {} }
+  void unlock() { lk_.clear(std::memory_order_release); }
+  std::atomic_flag lk_ = ATOMIC_FLAG_INIT;
+  bool pinned_ = false;
+  uint8_t* slab_ = nullptr;
+  size_t left_ = 0;
+  void* free_[kClasses] = {};
+};
+
 // --------------------------------------------------------------------- aligned storage ----
 template <typename T>
 struct Align16 {
   using value_type = T;
   Align16() = default;
   template <typename U> Align16(const Align16<U>&) {}
-  // malloc already returns 16-byte aligned blocks on x86-64 (alignof(max_align_t) = 16 there;
-  // this host code is built for x86-64 only): the aligned operator new would take glibc's
-  // memalign path, which bypasses the per-thread cache -- every payload, packet and result buffer
-  // of the batching adaptor is one of these
-  T* allocate(size_t n)
-  {
-    void* p = std::malloc(n * sizeof(T) ? n * sizeof(T) : 1);
-    if (!p) throw std::bad_alloc();
-    return static_cast<T*>(p);
-  }
-  void deallocate(T* p, size_t) { std::free(p); }
+  // blocks of BlockPool: pinned when a device is present, else malloc's (16-byte aligned on
+  // x86-64; glibc's memalign path, which the aligned operator new takes, bypasses its thread cache)
+  T* allocate(size_t n) { return static_cast<T*>(BlockPool::get().alloc(n * sizeof(T))); }
+  void deallocate(T* p, size_t n) { BlockPool::get().release(p, n * sizeof(T)); }
   // resize(n) default-initialises (no zeroing), like the reference's byte_buffer (buffer.hh:66-73);
   // resize(n, 0) and assign(n, 0) still zero-fill
   template <typename U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
@@ -115,6 +214,7 @@ struct DevChunk {
 struct Node;
 using NodeRef = std::shared_ptr<Node>;
 constexpr uint32_t kNoPos = ~0u;
+constexpr uint32_t kDirect = ~0u - 1;     // a root's result goes straight into its own pinned buffer
 // c * (the first len bytes of node's payload, zero-extended)
 struct Term {
   NodeRef node;
@@ -425,8 +525,12 @@ class Device {
   {
     NTC_PROF_T(t_stage);
     const uint64_t up_mark = ep + (1ull << 63);
-    std::vector<Node*> up;
-    size_t up_bytes = 0, out_bytes = 0, nterms = 0;
+    // new payloads: in pinned blocks the device pulls them itself (upload jobs), others are
+    // staged into the flush's copy
+    BlockPool& pool = BlockPool::get();
+    std::vector<Node*> up, pull;
+    size_t up_bytes = 0, pull_bytes = 0, out_bytes = 0, nterms = 0;
+    uint32_t pull_max = 1;
     for (Node* n : todo) {
       nterms += n->expr.size();
       out_bytes += pad16(n->size);
@@ -434,21 +538,34 @@ class Device {
         Node* c = t.node.get();
         if (c->chunk || (c->derived && !c->done) || c->mark == up_mark) continue;
         c->mark = up_mark;
-        up.push_back(c);
-        up_bytes += pad16(c->size);
+        if (pool.pooled(c->host.capacity()) && c->size) {
+          pull.push_back(c);
+          pull_bytes += pad16(c->size);
+          pull_max = std::max<uint32_t>(pull_max, c->size);
+        } else {
+          up.push_back(c);
+          up_bytes += pad16(c->size);
+        }
       }
     }
-    // results the host needs: roots evaluated now (second output) and earlier (device copy)
+    // results the host needs: roots evaluated now (second output: straight into the node's own
+    // pinned buffer, or the staging set's results) and earlier (device copy)
     size_t root_bytes = 0, late_bytes = 0;
     std::vector<Node*> late;
     for (Node* r : roots) {
       if (!r->derived || r->fetched) continue;
+      const bool direct = pool.pinned();
+      if (direct) r->host.resize(r->size);         // a pooled block (sizes <= 65535)
       if (!r->done) {
-        r->rpos = static_cast<uint32_t>(root_bytes);
-        root_bytes += pad16(r->size);
+        if (direct) {
+          r->rpos = kDirect;
+        } else {
+          r->rpos = static_cast<uint32_t>(root_bytes);
+          root_bytes += pad16(r->size);
+        }
       } else if (r->chunk) {
         late.push_back(r);
-        late_bytes += pad16(r->size);
+        if (!direct) late_bytes += pad16(r->size);
       }
     }
     if (todo.empty() && late.empty()) return 0;
@@ -461,9 +578,11 @@ class Device {
       complete_oldest_locked();
     }
     Stage& S = st_[si];
-    // flush region of the arena: [uploaded payloads | descriptors | job outputs]
-    const size_t desc = pad16(todo.size() * sizeof(ntc_gf256_gather_job) + nterms * sizeof(ntc_gf256_gather_term));
-    const size_t region = up_bytes + (todo.empty() ? 0 : desc) + out_bytes;
+    // flush region of the arena: [staged payloads | descriptors | pulled payloads | job outputs];
+    // descriptors: the upload jobs (one term each) first, then the combination jobs
+    const size_t npull = pull.size(), njobs = npull + todo.size();
+    const size_t desc = pad16(njobs * sizeof(ntc_gf256_gather_job) + (npull + nterms) * sizeof(ntc_gf256_gather_term));
+    const size_t region = up_bytes + (todo.empty() ? 0 : desc) + pull_bytes + out_bytes;
     size_t base = 0;
     DevChunk* ch = region ? arena_alloc(region, &base) : nullptr;
     grow_stage(S, up_bytes + desc, root_bytes + late_bytes);
@@ -479,18 +598,29 @@ class Device {
       pos += pad16(c->size);
     }
     auto* jobs = reinterpret_cast<ntc_gf256_gather_job*>(h_up + up_bytes);
-    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_up + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
+    auto* terms = reinterpret_cast<ntc_gf256_gather_term*>(h_up + up_bytes + njobs * sizeof(ntc_gf256_gather_job));
     size_t ti = 0, opos = base + up_bytes + desc;
+    for (size_t j = 0; j < npull; ++j) {           // upload jobs: 1 * the payload, read over PCIe once
+      Node* c = pull[j];
+      c->chunk = ch;
+      c->off = static_cast<uint32_t>(opos);
+      ch->live.fetch_add(1, std::memory_order_relaxed);
+      opos += pad16(c->size);
+      jobs[j] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + c->off), 0, static_cast<uint32_t>(ti), 1,
+                                     c->size, 0};
+      terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(c->data()), c->size, 1};
+    }
     for (size_t j = 0; j < todo.size(); ++j) {
       Node* n = todo[j];
       n->chunk = ch;
       n->off = static_cast<uint32_t>(opos);
       ch->live.fetch_add(1, std::memory_order_relaxed);
       opos += pad16(n->size);
-      const uint64_t out2 = n->rpos != kNoPos ? reinterpret_cast<uint64_t>(h_down + n->rpos) : 0;
-      jobs[j] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + n->off), out2,
-                                     static_cast<uint32_t>(ti), static_cast<uint32_t>(n->expr.size()),
-                                     n->size, 0};
+      const uint64_t out2 = n->rpos == kDirect ? reinterpret_cast<uint64_t>(n->host.data())
+                          : n->rpos != kNoPos ? reinterpret_cast<uint64_t>(h_down + n->rpos) : 0;
+      jobs[npull + j] = ntc_gf256_gather_job{reinterpret_cast<uint64_t>(ch->d + n->off), out2,
+                                             static_cast<uint32_t>(ti), static_cast<uint32_t>(n->expr.size()),
+                                             n->size, 0};
       for (const Term& t : n->expr)
         terms[ti++] = ntc_gf256_gather_term{reinterpret_cast<uint64_t>(t.node->chunk->d + t.node->off),
                                             std::min<uint32_t>(t.len, n->size), t.c};
@@ -508,17 +638,25 @@ class Device {
       check(hipMemcpyAsync(ch->d + base, h_up, up_bytes + desc, hipMemcpyHostToDevice, stream_), "H2D payloads + jobs");
     const auto* djobs = reinterpret_cast<const ntc_gf256_gather_job*>(todo.empty() ? nullptr : ch->d + base + up_bytes);
     const auto* dterms = reinterpret_cast<const ntc_gf256_gather_term*>(
-        todo.empty() ? nullptr : ch->d + base + up_bytes + todo.size() * sizeof(ntc_gf256_gather_job));
+        todo.empty() ? nullptr : ch->d + base + up_bytes + njobs * sizeof(ntc_gf256_gather_job));
+    if (npull && ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(npull), djobs, dterms, pull_max, stream_))
+      throw device_error(ntc_gf256_last_error());
     for (size_t a = 0; a < todo.size();) {
       size_t b = a;
       uint32_t m = 1;
       while (b < todo.size() && todo[b]->level == todo[a]->level) m = std::max<uint32_t>(m, todo[b++]->size);
-      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(b - a), djobs + a, dterms, m, stream_))
+      if (ntc_gf256_gather_combine(eng_, static_cast<uint32_t>(b - a), djobs + npull + a, dterms, m, stream_))
         throw device_error(ntc_gf256_last_error());
       a = b;
     }
     size_t lp = root_bytes;
     for (Node* r : late) {
+      if (pool.pinned()) {                       // straight into the node's pinned buffer
+        r->rpos = kDirect;
+        if (r->size)
+          check(hipMemcpyAsync(r->host.data(), r->chunk->d + r->off, r->size, hipMemcpyDeviceToHost, stream_), "D2H");
+        continue;
+      }
       r->rpos = static_cast<uint32_t>(lp);
       check(hipMemcpyAsync(h_down + lp, r->chunk->d + r->off, pad16(r->size), hipMemcpyDeviceToHost, stream_), "D2H");
       lp += pad16(r->size);
@@ -611,8 +749,8 @@ class Device {
     for (auto& rp : f.roots) {
       Node* r = rp.first.get();
       if (r->fetched) continue;
-      r->host.assign(S.down + rp.second, S.down + rp.second + r->size);
-      r->hoff = 0;
+      if (rp.second != kDirect) r->host.assign(S.down + rp.second, S.down + rp.second + r->size);
+      r->hoff = 0;                               // (kDirect: the job wrote the node's own buffer)
       r->fetched = true;
     }
     NTC_PROF_ADD(complete, t_c);

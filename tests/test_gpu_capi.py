@@ -145,19 +145,27 @@ def test_rejects_wrong_packet_types(capi):
     assert e.value.kind == "overflow_error"
 
 
-@pytest.mark.parametrize("mode", ["immediate", "batched"])
+@pytest.mark.parametrize("mode", ["immediate", "batched", "async", "batched-unpinned", "async-unpinned"])
 @pytest.mark.parametrize("flows,items,size,window,rate,loss", [(16, 24, 1024, 32, 4, 10),
-                                                               (5, 40, 300, 8, 2, 30)])
+                                                               (5, 40, 300, 8, 2, 30),
+                                                               (7, 30, 4000, 16, 3, 20)])
 def test_c_level_per_packet_matches_oracle(oracle, mode, flows, items, size, window, rate, loss):
     """tools/pp_driver.c (bench.py --per-packet's C-level GPU leg: one encoder / decoder per
-    flow through the reference C ABI, immediate or batched) produces exactly the packets and the
-    deliveries of the oracle's or_pp_bench on the same payload and loss draws."""
+    flow through the reference C ABI, immediate, batched or batched with asynchronous flushes)
+    produces exactly the packets and the deliveries of the oracle's or_pp_bench on the same payload
+    and loss draws -- with the payloads in pinned pool blocks that the device reads and writes
+    directly (default) and in malloc'd buffers staged through the flush's copies
+    (NTC_BATCH_UNPINNED=1, "-unpinned")."""
     import ctypes as C
     import subprocess
     drv = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "_build",
                        "pp_driver")
     args = [str(x) for x in (flows, items, size, window, rate, loss, 11)]
-    r = subprocess.run([drv, mode] + args, capture_output=True, text=True, timeout=120)
+    env = dict(os.environ)
+    if mode.endswith("-unpinned"):
+        mode = mode[:-len("-unpinned")]
+        env["NTC_BATCH_UNPINNED"] = "1"
+    r = subprocess.run([drv, mode] + args, capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr
     g = json.loads(r.stdout.strip().splitlines()[-1])
     secs, cnt, hs = (C.c_double * 2)(), (C.c_uint64 * 4)(), (C.c_uint64 * 2)()

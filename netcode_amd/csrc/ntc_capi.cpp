@@ -1502,8 +1502,20 @@ class Decoder {
     uint16_t esz;
     bytes sym;                   // immediate mode
     uint16_t symsz;
-    Expr red;                    // batch mode: the reduced repair, its own payload first
+    // batch mode: the reduced repair, its own payload first (held); the removed sources' terms do
+    // not hold them -- every such source has an id >= first, and the decoder keeps the sources it
+    // drops while a repair with a smaller or equal first id is alive (grave_)
+    Expr red;
+    uint32_t first = 0;          // the repair's first source id on the wire
   };
+  // the terms of r.red, each holding its node (for an expression that outlives the repair)
+  static Expr held(const Expr& red)
+  {
+    Expr e;
+    e.reserve(red.size());
+    for (const Term& t : red) e.push_back(Term{t.hold ? t.hold : t.node->shared_from_this(), t.c, t.len});
+    return e;
+  }
 
   void queue(Pending&& p);
  public:
@@ -1513,14 +1525,15 @@ class Decoder {
   NodeRef repair_node(const Rep& r) const
   {
     if (r.red.size() == 1 && r.red[0].c == 1 && r.red[0].len >= r.symsz) return r.red[0].hold;
-    return derived_node(f_.w, r.symsz, Expr(r.red));
+    return derived_node(f_.w, r.symsz, held(r.red));
   }
   // batch mode: c * (the reduced repair truncated to len), zero-extended to size bytes
   NodeRef scaled_repair(const Rep& r, uint32_t c, uint16_t len, uint16_t size) const
   {
     Expr e;
     e.reserve(r.red.size());
-    for (const Term& t : r.red) e.push_back(Term{t.hold, f_.mul(t.c, c), std::min(t.len, len)});
+    for (const Term& t : r.red)
+      e.push_back(Term{t.hold ? t.hold : t.node->shared_from_this(), f_.mul(t.c, c), std::min(t.len, len)});
     return derived_node(f_.w, size, std::move(e));
   }
 
@@ -1595,7 +1608,7 @@ class Decoder {
         const uint32_t c = f_.coef(r.id, s->id);
         if (same && s->size == sz0) cx ^= c;
         else r.esz = static_cast<uint16_t>(f_.msize(s->size, c) ^ r.esz);
-        r.red.push_back(Term{s->node, c, std::min<uint16_t>(s->size, r.symsz)});
+        r.red.push_back(Term{s->node.get(), c, std::min<uint16_t>(s->size, r.symsz)});   // unheld
       }
       if (cx) r.esz = static_cast<uint16_t>(f_.msize(sz0, cx) ^ r.esz);
       return;
@@ -1672,7 +1685,7 @@ class Decoder {
         missing_[sid].insert(id);
         remaining.push_back(sid);
       }
-    Rep& r = repairs_.emplace(id, Rep{id, std::move(remaining), esz, bytes(), symsz, {}}).first->second;
+    Rep& r = repairs_.emplace(id, Rep{id, std::move(remaining), esz, bytes(), symsz, {}, ids.front()}).first->second;
     if (batch_) {
       r.red.reserve(1 + known_.size());
       r.red.push_back(Term{own ? adopt_node(std::move(*own), sym - own->data(), symsz) : base_node(sym, symsz),
@@ -1758,8 +1771,30 @@ class Decoder {
       if (first_missing_ < id) first_missing_ = id;
       flush_ordered();
     }
-    sources_.erase(sources_.begin(), sources_.lower_bound(id));
+    // sources leaving: those a live repair's unheld terms may read (id >= its first id) wait in
+    // grave_ until no such repair is left
+    const auto cut = sources_.lower_bound(id);
+    uint32_t keep_from = ~0u;                      // smallest first id of a live repair
+    for (const auto& kv : repairs_) keep_from = std::min(keep_from, kv.second.first);
+    if (batch_)
+      for (auto it = sources_.begin(); it != cut; ++it)
+        if (it->first >= keep_from && it->second.node) grave_.push_back({it->first, std::move(it->second.node)});
+    sources_.erase(sources_.begin(), cut);
     missing_.erase(missing_.begin(), missing_.lower_bound(id));
+    prune_grave(keep_from);
+  }
+  void prune_grave(uint32_t keep_from)
+  {
+    if (grave_.empty()) return;
+    grave_.erase(std::remove_if(grave_.begin(), grave_.end(),
+                                [keep_from](const std::pair<uint32_t, NodeRef>& g) { return g.first < keep_from; }),
+                 grave_.end());
+  }
+  void prune_grave()
+  {
+    uint32_t keep_from = ~0u;
+    for (const auto& kv : repairs_) keep_from = std::min(keep_from, kv.second.first);
+    prune_grave(keep_from);
   }
 
   // detail/invert_matrix.cc:9-128 semantics: returns false on a singular matrix (the reference
@@ -1887,6 +1922,7 @@ class Decoder {
   ntc_data_handler dh_;
   std::vector<uint32_t> ids_;          // scratch of add_packet / on_repair
   std::vector<const Src*> known_;
+  std::vector<std::pair<uint32_t, NodeRef>> grave_;   // dropped sources live repairs may read
   uint32_t first_missing_ = 0;
   OrderedIds ordered_;
   FlatMap<uint32_t, Src> sources_;

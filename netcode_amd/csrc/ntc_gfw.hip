@@ -17,6 +17,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
 
 #include "engine.hh"
 #include "netcode/gpu.h"
@@ -145,6 +148,192 @@ __global__ __launch_bounds__(256) void gfw_combine(CombineArgs a, uint32_t nspan
           make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
+// Four-Russians form (round 6, the default): per input dword the 16 XOR combinations of each
+// group of four powers x*alpha^(4g) .. x*alpha^(4g+3) are built once (w - 1 xtime steps + 11 XORs
+// per group), and a row adds one table entry per group -- the entry chosen by the nibble of its
+// wave-uniform coefficient through VGPR-relative addressing (gfw_fr_lookup, generated by
+// tools/gen_gfw_fr.py).  Per (row, input dword): w/4 indexed XORs instead of the masked form's w
+// AND-XORs.  A lane owns D dwords (the table takes 16 * (w/4) * D VGPRs, <= 128).
+template <int W> struct FrGeom {
+  static constexpr int G = W / 4 > 0 ? W / 4 : 1;
+  static constexpr int D = W == 4 ? 4 : W == 32 ? 1 : 2;
+  static constexpr int NT = 16 * G * D;
+  static constexpr uint32_t SPAN = 256u * D;
+};
+
+#include "gfw_fr_lookup.inc"
+
+// a wave-uniform load through the scalar unit (constant address space)
+template <typename T>
+__device__ __forceinline__ T const_load(const void* p)
+{
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
+// alpha * x with every shift amount and mask in a VGPR (opaque to the compiler, so it cannot
+// fold them back into inline constants or SGPR operands, whose VALU forms issue at half rate on
+// gfx950 -- DESIGN §3 "Issue rates by instruction form")
+template <int W> struct XtimeV {
+  uint32_t a, b, k;        // w = 16: (1,1), (15,15), 0x100B100B; w = 32: 1, 31, 0x00400007
+  __device__ __forceinline__ XtimeV()
+  {
+    constexpr uint32_t A = W == 16 ? 0x00010001u : 1u, B = W == 16 ? 0x000F000Fu : 31u;
+    constexpr uint32_t K = W == 16 ? 0x100B100Bu : 0x00400007u;
+    asm volatile("v_mov_b32 %0, %3\n" "v_mov_b32 %1, %4\n" "v_mov_b32 %2, %5\n"
+                 : "=v"(a), "=v"(b), "=v"(k) : "i"(A), "i"(B), "i"(K));
+  }
+  __device__ __forceinline__ uint32_t operator()(uint32_t y) const
+  {
+    if constexpr (W == 16) {
+      typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+      typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+      const u16x2 sh = __builtin_bit_cast(u16x2, y) << __builtin_bit_cast(u16x2, a);
+      const i16x2 sg = __builtin_bit_cast(i16x2, y) >> __builtin_bit_cast(i16x2, b);
+      return __builtin_amdgcn_bitop3_b32(__builtin_bit_cast(uint32_t, sh), __builtin_bit_cast(uint32_t, sg), k, 0x78);
+    } else {
+      const uint32_t sg = static_cast<uint32_t>(static_cast<int32_t>(y) >> b);
+      return __builtin_amdgcn_bitop3_b32(y << a, sg, k, 0x78);
+    }
+  }
+};
+template <int W> struct XtimeC {      // w = 4, 8: the packed-byte forms as they are
+  __device__ __forceinline__ uint32_t operator()(uint32_t y) const { return xtime<W>(y); }
+};
+
+template <int D> struct LaneVec;
+template <> struct LaneVec<1> {
+  typedef uint32_t T;
+  static __device__ __forceinline__ void get(const T& v, uint32_t (&x)[1]) { x[0] = v; }
+  static __device__ __forceinline__ T make(const uint32_t (&x)[1]) { return x[0]; }
+};
+template <> struct LaneVec<2> {
+  typedef uint2 T;
+  static __device__ __forceinline__ void get(const T& v, uint32_t (&x)[2]) { x[0] = v.x; x[1] = v.y; }
+  static __device__ __forceinline__ T make(const uint32_t (&x)[2]) { return make_uint2(x[0], x[1]); }
+};
+template <> struct LaneVec<4> {
+  typedef uint4 T;
+  static __device__ __forceinline__ void get(const T& v, uint32_t (&x)[4])
+  {
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
+  static __device__ __forceinline__ T make(const uint32_t (&x)[4]) { return make_uint4(x[0], x[1], x[2], x[3]); }
+};
+
+// One wave per (generation, SPAN-byte column span, group of RB rows); a lane owns 4*D bytes.
+template <int W, int RB>
+__global__ __launch_bounds__(256) void gfw_combine_fr(CombineArgs a, uint32_t nspan, uint32_t ngrp)
+{
+  constexpr int G = FrGeom<W>::G, D = FrGeom<W>::D, NT = FrGeom<W>::NT;
+  typedef typename LaneVec<D>::T V;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t per_g = nspan * ngrp;
+  if (wave >= a.G * per_g) return;
+  const uint32_t g = wave / per_g, rem = wave % per_g;
+  const uint32_t span = rem % nspan, r0 = (rem / nspan) * RB;
+  const uint32_t col = span * FrGeom<W>::SPAN + 4u * D * lane;
+  const bool act = col < a.stride;                    // stride % 16 == 0: all D dwords or none
+  const uint32_t nr = a.rows - r0 < static_cast<uint32_t>(RB) ? a.rows - r0 : static_cast<uint32_t>(RB);
+  const uint8_t* in = a.in + static_cast<size_t>(g) * a.k * a.stride + (act ? col : 0u);
+  const uint32_t* cf = a.coef + static_cast<size_t>(g) * a.k * a.rows + r0;
+  uint32_t acc[RB][D];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[r][d] = 0;
+  // coefficients through the scalar unit, one input ahead (rows past the group's last read its
+  // last row's word and are zeroed)
+  typedef uint32_t CV __attribute__((ext_vector_type(RB)));
+  auto coefs = [&](uint32_t i, uint32_t (&c)[RB]) {
+    const uint32_t* p = cf + static_cast<size_t>(i) * a.rows;
+    if (nr == static_cast<uint32_t>(RB)) {             // the group's RB words in one scalar load
+      const CV v = const_load<CV>(p);
+#pragma unroll
+      for (int r = 0; r < RB; ++r) c[r] = v[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        c[r] = static_cast<uint32_t>(r) < nr ? const_load<uint32_t>(p + r) : 0u;
+    }
+  };
+  uint32_t cn[RB];
+  coefs(0, cn);
+  const typename std::conditional<(W >= 16), XtimeV<W>, XtimeC<W>>::type xtv;
+  // inputs PF ahead in registers (a wave's work per input is short next to the memory latency)
+  constexpr int PF = D == 4 ? 2 : 3;
+  V nx[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j)
+    nx[j] = act && static_cast<uint32_t>(j) < a.k ? *reinterpret_cast<const V*>(in + static_cast<size_t>(j) * a.stride) : V{};
+  for (uint32_t i = 0; i < a.k; ++i) {
+    uint32_t x[D];
+    LaneVec<D>::get(nx[0], x);
+#pragma unroll
+    for (int j = 0; j + 1 < PF; ++j) nx[j] = nx[j + 1];
+    if (act && i + PF < a.k) nx[PF - 1] = *reinterpret_cast<const V*>(in + static_cast<size_t>(i + PF) * a.stride);
+    uint32_t c[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) c[r] = cn[r];
+    if (i + 1 < a.k) coefs(i + 1, cn);
+    if constexpr (W < 32) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) c[r] &= (1u << W) - 1u;
+    }
+    uint32_t any = 0;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) any |= c[r];
+    if (any == 0) continue;                             // wave-uniform
+    uint32_t T[NT];
+    // the D dwords' power chains side by side (independent: each step of one hides the other's latency)
+    uint32_t y[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) y[d] = x[d];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          uint32_t* t = T + (d * G + q) * 16;
+          if (j == 0) t[0] = 0;
+          t[1 << j] = y[d];
+          if (j < 3 || q + 1 < G) y[d] = xtv(y[d]);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        uint32_t* t = T + (d * G + q) * 16;
+#ifdef NTC_GFW_ABL_NOTABLE
+#pragma unroll
+        for (int m = 0; m < 16; ++m) t[m] = x[d] + m;
+        continue;
+#endif
+        t[3] = t[1] ^ t[2];
+        t[5] = t[4] ^ t[1];
+        t[6] = t[4] ^ t[2];
+        t[7] = t[4] ^ t[3];
+#pragma unroll
+        for (int m = 1; m < 8; ++m) t[8 + m] = t[8] ^ t[m];
+      }
+    }
+#if defined(NTC_GFW_ABL_NOLOOKUP)    // timing-only ablations (tools/build_variant.sh -D...)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) asm volatile("" :: "v"(T[j]));
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[r][0] ^= c[r];
+#else
+    gfw_fr_lookup<W, RB>(acc, T, c);
+#endif
+  }
+  if (!act) return;
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+    if (static_cast<uint32_t>(r) < nr)
+      *reinterpret_cast<V*>(a.out + (static_cast<size_t>(g) * a.rows + r0 + r) * a.stride + col) =
+          LaneVec<D>::make(acc[r]);
+}
+
 // dst[0..len) = c * src (+ dst); word boundaries relative to the region start; a partial last word
 // reads missing bytes as zero and writes only bytes inside len.
 template <int W>
@@ -234,7 +423,12 @@ int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k
   if (stride == 0 || stride % 16 != 0) return fail(NTC_GPU_EINVAL, "stride must be a non-zero multiple of 16");
   // rows per wave: 8, or the next power of two covering fewer rows
   const uint32_t rb = rows >= 8 ? 8 : rows > 2 ? 4 : rows;
-  const uint32_t nspan = (stride + kGfwSpan - 1) / kGfwSpan, ngrp = (rows + rb - 1) / rb;
+  // NTC_GFW_KERNEL=mask: the masked shift-and-add form (round 4) instead of the table lookups
+  const char* form = std::getenv("NTC_GFW_KERNEL");
+  const bool fr = !(form && std::strcmp(form, "mask") == 0);
+  const uint32_t spanb = !fr ? kGfwSpan : w == 4 ? FrGeom<4>::SPAN : w == 8 ? FrGeom<8>::SPAN
+                       : w == 16 ? FrGeom<16>::SPAN : FrGeom<32>::SPAN;
+  const uint32_t nspan = (stride + spanb - 1) / spanb, ngrp = (rows + rb - 1) / rb;
   const uint64_t waves = static_cast<uint64_t>(G) * nspan * ngrp;
   const uint64_t blocks = (waves + 3) / 4;
   if (blocks > 0x7FFFFFFFull || waves > 0xFFFFFFFFull) return fail(NTC_GPU_EUNSUPPORTED, "batch too large for one launch");
@@ -243,7 +437,7 @@ int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k
   using Fn = void (*)(CombineArgs, uint32_t, uint32_t);
   Fn fn;
   switch (w * 16 + rb) {
-#define NTC_GFW_CASE(W_, RB_) case W_ * 16 + RB_: fn = gfw_combine<W_, RB_>; break;
+#define NTC_GFW_CASE(W_, RB_) case W_ * 16 + RB_: fn = fr ? gfw_combine_fr<W_, RB_> : gfw_combine<W_, RB_>; break;
     NTC_GFW_CASE(4, 1) NTC_GFW_CASE(4, 2) NTC_GFW_CASE(4, 4) NTC_GFW_CASE(4, 8)
     NTC_GFW_CASE(8, 1) NTC_GFW_CASE(8, 2) NTC_GFW_CASE(8, 4) NTC_GFW_CASE(8, 8)
     NTC_GFW_CASE(16, 1) NTC_GFW_CASE(16, 2) NTC_GFW_CASE(16, 4) NTC_GFW_CASE(16, 8)

@@ -33,12 +33,16 @@ def test_region_multiply(gpu, oracle, w):
 
 
 @pytest.mark.parametrize("w", WS)
-# row groups of 8 / 4 / 2 / 1 per wave, 1 KiB column spans (ragged last span), all-zero sources
+# row groups of 8 / 4 / 2 / 1 per wave, 256 B - 1 KiB column spans (ragged last span), all-zero
+# sources; both kernel forms: the table lookups (default) and the masked shift-and-add
 @pytest.mark.parametrize("G,k,rows,stride", [(3, 5, 2, 64), (2, 17, 4, 1504), (1, 1, 1, 16), (2, 6, 9, 2064),
-                                             (1, 3, 8, 1024), (4, 33, 3, 48), (1, 4, 19, 1040)])
-def test_combine_batch(gpu, oracle, w, G, k, rows, stride):
+                                             (1, 3, 8, 1024), (4, 33, 3, 48), (1, 4, 19, 1040),
+                                             (2, 7, 16, 272), (1, 9, 5, 528)])
+@pytest.mark.parametrize("form", ["fr", "mask"])
+def test_combine_batch(gpu, oracle, monkeypatch, w, G, k, rows, stride, form):
     import torch
     from netcode_amd import combine
+    monkeypatch.setenv("NTC_GFW_KERNEL", form)
     rng = np.random.default_rng(G * 100 + k + w)
     x = rng.integers(0, 256, (G, k, stride), dtype=np.uint8)
     cf = rng.integers(0, cmax(w), (G, k, rows), dtype=np.uint64, endpoint=True).astype(np.uint32)

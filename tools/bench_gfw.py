@@ -1,4 +1,5 @@
-"""Throughput of the GF(2^w) batched combine (ntc_gf_combine_batch, w in {4, 8, 16, 32}) at the
+"""Throughput of the GF(2^w) batched combine (both kernel forms: the table lookups and the masked
+shift-and-add, NTC_GFW_KERNEL) (ntc_gf_combine_batch, w in {4, 8, 16, 32}) at the
 config-2 shape (k=32 inputs -> 8 outputs, 1 KiB symbols, G=4096), HIP events on the engine's
 stream; prints one JSON line.  For comparison the GF(2^8)-dedicated batch kernels run the same
 shape (ntc_gf256_combine_batch).  bytes/launch = inputs read + outputs written.
@@ -31,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--G", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--w", type=int, nargs="*", default=[4, 8, 16, 32])
+    ap.add_argument("--forms", nargs="*", default=["fr", "mask"])
     a = ap.parse_args()
     from netcode_amd import _native, combine
     from netcode_amd.engine import Engine
@@ -41,13 +44,29 @@ def main():
     s = torch.cuda.current_stream(dev)
     nbytes = G * (k + rows) * S
     out = {}
-    for w in (4, 8, 16, 32):
+    for w in a.w:
         hi = (1 << w) - 1 if w < 32 else 2 ** 31 - 1
         cf = torch.randint(1, hi, (G, k, rows), dtype=torch.int64, device=dev, generator=g).to(torch.int32)
-        o = combine(w, x, cf)
-        t = timed(lambda: combine(w, x, cf, o), a.reps, s)
-        out[f"w{w}"] = {"ms": round(t, 4), "GBps": round(nbytes / t / 1e6, 1),
-                        "elem_MAC_T_per_s": round(G * k * rows * S * 8 / w / t / 1e9, 2)}
+        res = {}
+        # both kernel forms, interleaved twice: table lookups (default) and masked shift-and-add;
+        # their outputs must agree
+        for rep in range(2):
+            for form in a.forms:
+                os.environ["NTC_GFW_KERNEL"] = form
+                o = combine(w, x, cf)
+                t = timed(lambda: combine(w, x, cf, o), a.reps, s)
+                res.setdefault(form, []).append(t)
+                res.setdefault(form + "_out", o)
+        os.environ.pop("NTC_GFW_KERNEL", None)
+        same = bool(torch.equal(res["fr_out"], res["mask_out"])) if len(a.forms) == 2 else None
+        for form in a.forms:
+            t = min(res[form])
+            out[f"w{w}" + ("" if form == "fr" else "_mask")] = {
+                "ms": round(t, 4), "GBps": round(nbytes / t / 1e6, 1),
+                "elem_MAC_T_per_s": round(G * k * rows * S * 8 / w / t / 1e9, 2),
+                "all_ms": [round(v, 4) for v in res[form]]}
+        if same is not None:
+            out[f"w{w}"]["forms_bit_exact"] = same
     # the dedicated GF(2^8) path on the same shape
     L = _native.load()
     eng = Engine.get(dev)

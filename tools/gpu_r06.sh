@@ -51,6 +51,9 @@ for s in "${S[@]}"; do
       run gather_cur 300 python -u -m pytest $T -q -m gpu --timeout 120 --timeout-method thread
       cp "$AB_OTHER" netcode_amd/libntc_gf256.so
       run gather_other 300 python -u -m pytest $T -q -m gpu --timeout 120 --timeout-method thread ;;
+    gfw)       # GF(2^w) parity (both kernel forms), then both forms timed interleaved
+      run gfw_tests 300 python -u -m pytest tests/test_gpu_gfw.py -x -q -m gpu --timeout 120 --timeout-method thread
+      run gfw_bench 300 python tools/bench_gfw.py ;;
     gfwab)     # GF(2^w) parity, then tools/bench_gfw.py interleaved against $AB_OTHER
       run gfw_tests 300 python -u -m pytest tests/test_gpu_gfw.py -x -q -m gpu --timeout 120 --timeout-method thread
       for rep in 1 2; do

@@ -23,6 +23,7 @@ if [ "$PART" = A ]; then
   # more region-MAC work per packet: 4 KiB payloads; a repair every 2 sources
   step per_packet_s4096 400 python bench.py --per-packet --pp-reps 3 --size 4096 --c-items 64
   step per_packet_rate2 400 python bench.py --per-packet --pp-reps 3 --rate 2
+  step gfw_bench 300 python tools/bench_gfw.py
 else
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --no-cpu-baseline --no-host-rate > $OUT/trace.log 2>&1) || { tail -20 $OUT/trace.log; exit 1; }
   echo "trace done"

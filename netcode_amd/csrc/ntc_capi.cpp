@@ -51,9 +51,12 @@ struct device_error : std::runtime_error {
 // block of pinned host memory when a HIP device is present: the GPU then reads a new payload
 // straight from the buffer the application filled (an upload job of the flush's first launch, one
 // PCIe read) and writes each result straight into the buffer its node keeps -- no staging copy
-// in, no copy out (DESIGN.md §3 batching; CPU access to these blocks runs at the speed of
-// malloc'd memory, tools/pinned_probe.hip).  Size classes: n rounded up to 1/8 of its power of
-// two (64 B .. 128 KiB), carved from 4 MiB hipHostMalloc slabs that are never returned (the
+// in, no copy out (DESIGN.md §3 batching).  The slabs are malloc'd pages pinned by
+// hipHostRegister, so they sit on the NUMA node of the CPU thread that touches every byte:
+// hipHostMalloc places them on the GPU's node, which on a box whose CPUs are on the other socket
+// made CPU reads 25 % slower (tools/pinned_probe.hip); the GPU reads either over PCIe at the same
+// rate.  Size classes: n rounded up to 1/8 of its power of
+// two (64 B .. 128 KiB), carved from 4 MiB slabs that are never returned (the
 // adaptor's peak payload memory stays reserved for the process); larger buffers, and every buffer
 // without a device (or in the host-stub build), are malloc'd.  A spin lock guards the free lists.
 class BlockPool {
@@ -104,8 +107,13 @@ class BlockPool {
 #ifndef NTC_CAPI_HOST_STUB
     int n = 0;
     void* p = nullptr;
+    // NTC_BATCH_PINNED_NUMA=gpu: slabs from hipHostMalloc, whose pages sit on the GPU's NUMA node
+    // (A/B switch); default: malloc'd slabs pinned by hipHostRegister, so their pages are faulted
+    // in on the NUMA node of the thread that first needs the pool -- the CPU side's node
+    const char* numa = std::getenv("NTC_BATCH_PINNED_NUMA");
+    gpu_node_ = numa && std::strcmp(numa, "gpu") == 0;
     if (std::getenv("NTC_BATCH_UNPINNED") == nullptr && hipGetDeviceCount(&n) == hipSuccess && n > 0 &&
-        hipHostMalloc(&p, kSlab, hipHostMallocDefault) == hipSuccess) {
+        (p = new_slab()) != nullptr) {
       slab_ = static_cast<uint8_t*>(p);
       left_ = kSlab;
       pinned_ = true;
@@ -132,8 +140,8 @@ class BlockPool {
   {
 #ifndef NTC_CAPI_HOST_STUB
     if (left_ < b) {                           // a new slab (the old one's tail, < 128 KiB, stays unused)
-      void* p = nullptr;
-      if (hipHostMalloc(&p, kSlab, hipHostMallocDefault) != hipSuccess) return nullptr;
+      void* p = new_slab();
+      if (!p) return nullptr;
       slab_ = static_cast<uint8_t*>(p);
       left_ = kSlab;
     }
@@ -143,10 +151,36 @@ class BlockPool {
     left_ -= b;
     return r;
   }
+#ifndef NTC_CAPI_HOST_STUB
+  // a 4 MiB slab the device reads and writes through the same address as the host (on the CPU
+  // thread's NUMA node unless gpu_node_; hipHostMalloc when registering is refused or maps the
+  // pages at another device address)
+  void* new_slab()
+  {
+    void* p = nullptr;
+    if (!gpu_node_) {
+      p = std::aligned_alloc(4096, kSlab);
+      if (p && hipHostRegister(p, kSlab, hipHostRegisterMapped) == hipSuccess) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess && dp == p) return p;
+        (void)hipHostUnregister(p);
+      }
+      (void)hipGetLastError();
+      std::free(p);
+      p = nullptr;
+    }
+    if (hipHostMalloc(&p, kSlab, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return p;
+  }
+#endif
   void lock() { while (lk_.test_and_set(std::memory_order_acquire)) {} }
   void unlock() { lk_.clear(std::memory_order_release); }
   std::atomic_flag lk_ = ATOMIC_FLAG_INIT;
   bool pinned_ = false;
+  bool gpu_node_ = false;
   uint8_t* slab_ = nullptr;
   size_t left_ = 0;
   void* free_[kClasses] = {};

@@ -46,7 +46,8 @@ size_t ntc_decoder_counter(const ntc_decoder_t* dec, int which) NTC_C_NOEXCEPT N
  * Deleting an attached object discards its queued events; deleting a batch discards every queued
  * event and detaches its objects.  Memory: with a device present, data, packet and payload buffers
  * are pinned host blocks from a process-wide pool that keeps its peak size (the device reads new
- * payloads and writes results there directly); NTC_BATCH_UNPINNED=1 selects malloc'd buffers. */
+ * payloads and writes results there directly; the pages sit on the calling CPU's NUMA node);
+ * NTC_BATCH_UNPINNED=1 selects malloc'd buffers. */
 typedef struct ntc_batch_t ntc_batch_t;
 ntc_batch_t* ntc_new_batch(void) NTC_C_NOEXCEPT;
 void ntc_delete_batch(ntc_batch_t* batch) NTC_C_NOEXCEPT;   /* NULL is a no-op */

@@ -145,7 +145,8 @@ def test_rejects_wrong_packet_types(capi):
     assert e.value.kind == "overflow_error"
 
 
-@pytest.mark.parametrize("mode", ["immediate", "batched", "async", "batched-unpinned", "async-unpinned"])
+@pytest.mark.parametrize("mode", ["immediate", "batched", "async", "batched-unpinned", "async-unpinned",
+                                  "async-gpunode"])
 @pytest.mark.parametrize("flows,items,size,window,rate,loss", [(16, 24, 1024, 32, 4, 10),
                                                                (5, 40, 300, 8, 2, 30),
                                                                (7, 30, 4000, 16, 3, 20)])
@@ -155,7 +156,8 @@ def test_c_level_per_packet_matches_oracle(oracle, mode, flows, items, size, win
     produces exactly the packets and the deliveries of the oracle's or_pp_bench on the same payload
     and loss draws -- with the payloads in pinned pool blocks that the device reads and writes
     directly (default) and in malloc'd buffers staged through the flush's copies
-    (NTC_BATCH_UNPINNED=1, "-unpinned")."""
+    (NTC_BATCH_UNPINNED=1, "-unpinned"); "-gpunode": the pool's slabs from hipHostMalloc instead of
+    registered malloc pages (NTC_BATCH_PINNED_NUMA=gpu)."""
     import ctypes as C
     import subprocess
     drv = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "_build",
@@ -165,6 +167,9 @@ def test_c_level_per_packet_matches_oracle(oracle, mode, flows, items, size, win
     if mode.endswith("-unpinned"):
         mode = mode[:-len("-unpinned")]
         env["NTC_BATCH_UNPINNED"] = "1"
+    if mode.endswith("-gpunode"):               # pool slabs from hipHostMalloc (the GPU's NUMA node)
+        mode = mode[:-len("-gpunode")]
+        env["NTC_BATCH_PINNED_NUMA"] = "gpu"
     r = subprocess.run([drv, mode] + args, capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr
     g = json.loads(r.stdout.strip().splitlines()[-1])

@@ -148,9 +148,9 @@ __global__ __launch_bounds__(256) void gfw_combine(CombineArgs a, uint32_t nspan
           make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
 }
 
-// Four-Russians form (round 6, the default): per input dword the 16 XOR combinations of each
-// group of four powers x*alpha^(4g) .. x*alpha^(4g+3) are built once (w - 1 xtime steps + 11 XORs
-// per group), and a row adds one table entry per group -- the entry chosen by the nibble of its
+// Four-Russians form (round 6, the default for groups of 8 rows): per input dword the 16 XOR
+// combinations of each group of four powers x*alpha^(4g) .. x*alpha^(4g+3) are built once (w - 1
+// xtime steps + 11 XORs per group), and a row adds one table entry per group -- the entry chosen by the nibble of its
 // wave-uniform coefficient through VGPR-relative addressing (gfw_fr_lookup, generated by
 // tools/gen_gfw_fr.py).  Per (row, input dword): w/4 indexed XORs instead of the masked form's w
 // AND-XORs.  A lane owns D dwords (the table takes 16 * (w/4) * D VGPRs, <= 128).
@@ -423,9 +423,12 @@ int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k
   if (stride == 0 || stride % 16 != 0) return fail(NTC_GPU_EINVAL, "stride must be a non-zero multiple of 16");
   // rows per wave: 8, or the next power of two covering fewer rows
   const uint32_t rb = rows >= 8 ? 8 : rows > 2 ? 4 : rows;
-  // NTC_GFW_KERNEL=mask: the masked shift-and-add form (round 4) instead of the table lookups
+  // the table lookups pay for their table build only over a full group of 8 rows: with 1, 2 or 4
+  // rows per wave the masked form is as fast or faster (profiles/r06/gfw/rows_1_2_4.txt; the per-packet
+  // C ABI combines one row per generation).  NTC_GFW_KERNEL=mask / fr forces one form.
   const char* form = std::getenv("NTC_GFW_KERNEL");
-  const bool fr = !(form && std::strcmp(form, "mask") == 0);
+  const bool fr = form && std::strcmp(form, "mask") == 0 ? false
+                : form && std::strcmp(form, "fr") == 0 ? true : rb == 8;
   const uint32_t spanb = !fr ? kGfwSpan : w == 4 ? FrGeom<4>::SPAN : w == 8 ? FrGeom<8>::SPAN
                        : w == 16 ? FrGeom<16>::SPAN : FrGeom<32>::SPAN;
   const uint32_t nspan = (stride + spanb - 1) / spanb, ngrp = (rows + rb - 1) / rb;

@@ -34,11 +34,13 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--w", type=int, nargs="*", default=[4, 8, 16, 32])
     ap.add_argument("--forms", nargs="*", default=["fr", "mask"])
+    ap.add_argument("--rows", type=int, default=8)
+    ap.add_argument("--no-gf256", action="store_true")
     a = ap.parse_args()
     from netcode_amd import _native, combine
     from netcode_amd.engine import Engine
     dev = torch.device("cuda", 0)
-    G, k, rows, S = a.G, 32, 8, 1024
+    G, k, rows, S = a.G, 32, a.rows, 1024
     g = torch.Generator(device=dev).manual_seed(1)
     x = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=g)
     s = torch.cuda.current_stream(dev)

@@ -144,6 +144,37 @@ def test_batched_decoders_match_unbatched(capi, oracle, w, in_order, seed):
     assert b.nb_decoded > 0
 
 
+@pytest.mark.parametrize("seed", range(20, 32))
+def test_batched_decoders_random_streams(capi, oracle, seed):
+    """Random windows (small ones make the decoder drop outdated sources and repairs while reduced
+    repairs still name them), repair rates, losses and reorderings, synchronous or asynchronous
+    flushes at random points: deliveries and packets equal the oracle's."""
+    rng = np.random.default_rng(seed)
+    window, rate = int(rng.integers(2, 48)), int(rng.integers(1, 7))
+    pkts = _lossy_stream(oracle, 8, seed, n=160, p_loss=float(rng.uniform(0.05, 0.4)), rate=rate,
+                         window=window)
+    in_order = bool(rng.integers(0, 2))
+    batch = capi.Batch(eager=bool(rng.integers(0, 2)), asynchronous=bool(rng.integers(0, 2)))
+    a = capi.Decoder(8, in_order=in_order)
+    o = oracle.Decoder(in_order=in_order, galois_field_size=8)
+    nb = int(rng.integers(4, 64))
+    for d in (a, o):
+        d.set_ack_period_ms(0)
+        d.set_ack_nb_packets(nb)
+    a.set_batch(batch)
+    for p in pkts:
+        a.add_packet(p)
+        o.add_packet(p)
+        if rng.random() < 0.15:
+            batch.flush()
+    while True:
+        batch.flush()
+        if batch.pending == 0:
+            break
+    assert a.data == [d for _, d in o.data]
+    assert a.packets == o.packets
+
+
 def test_batch_switching_and_shared_batch(capi, oracle):
     """Encoders and decoders on one batch; a decoder leaves batch mode mid-stream (its symbols are
     materialised) and keeps decoding identically."""

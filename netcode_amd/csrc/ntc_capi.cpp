@@ -79,9 +79,22 @@ class BlockPool {
     }
     const int c = cls(n);
     lock();
-    void* p = free_[c];
-    if (p) free_[c] = *static_cast<void**>(p);
-    else p = carve(csize(c));
+    void* p;
+    if (!free_[c].empty()) {
+      p = free_[c].back();
+      free_[c].pop_back();
+    } else {
+      p = carve(csize(c));
+      // room for every block of the class on its free list, so release() never allocates
+      if (p && ++carved_[c] > free_[c].capacity()) {
+        try {
+          free_[c].reserve(2 * carved_[c]);
+        } catch (...) {
+          unlock();
+          throw;
+        }
+      }
+    }
     unlock();
     if (!p) throw std::bad_alloc();
     return p;
@@ -94,9 +107,8 @@ class BlockPool {
     }
     const int c = cls(n);
     lock();
-    *static_cast<void**>(p) = free_[c];
-    free_[c] = p;
-    unlock();
+    free_[c].push_back(p);     // (the free lists live outside the blocks: taking a block touches
+    unlock();                  // none of its cold bytes)
   }
 
  private:
@@ -183,7 +195,8 @@ class BlockPool {
   bool gpu_node_ = false;
   uint8_t* slab_ = nullptr;
   size_t left_ = 0;
-  void* free_[kClasses] = {};
+  std::vector<void*> free_[kClasses];
+  size_t carved_[kClasses] = {};
 };
 
 // --------------------------------------------------------------------- aligned storage ----

@@ -421,14 +421,17 @@ int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k
   if (!valid_w(w)) return fail(NTC_GPU_EINVAL, "w must be 4, 8, 16 or 32");
   if (G == 0 || k == 0 || rows == 0) return fail(NTC_GPU_EINVAL, "G, k and rows must be > 0");
   if (stride == 0 || stride % 16 != 0) return fail(NTC_GPU_EINVAL, "stride must be a non-zero multiple of 16");
-  // rows per wave: 8, or the next power of two covering fewer rows
-  const uint32_t rb = rows >= 8 ? 8 : rows > 2 ? 4 : rows;
+  // rows per wave: 8, or the next power of two covering fewer rows (16 for the table lookups)
+  const uint32_t rbm = rows >= 8 ? 8 : rows > 2 ? 4 : rows;
   // the table lookups pay for their table build only over a full group of 8 rows: with 1, 2 or 4
   // rows per wave the masked form is as fast or faster (profiles/r06/gfw/rows_1_2_4.txt; the per-packet
   // C ABI combines one row per generation).  NTC_GFW_KERNEL=mask / fr forces one form.
   const char* form = std::getenv("NTC_GFW_KERNEL");
   const bool fr = form && std::strcmp(form, "mask") == 0 ? false
-                : form && std::strcmp(form, "fr") == 0 ? true : rb == 8;
+                : form && std::strcmp(form, "fr") == 0 ? true : rbm == 8;
+  // with 16 rows or more the lookups take 16 rows per wave: the table build is shared by twice
+  // the rows (176 VGPRs at w = 16: 2 waves per SIMD)
+  const uint32_t rb = fr && rows >= 16 ? 16 : rbm;
   const uint32_t spanb = !fr ? kGfwSpan : w == 4 ? FrGeom<4>::SPAN : w == 8 ? FrGeom<8>::SPAN
                        : w == 16 ? FrGeom<16>::SPAN : FrGeom<32>::SPAN;
   const uint32_t nspan = (stride + spanb - 1) / spanb, ngrp = (rows + rb - 1) / rb;
@@ -439,13 +442,15 @@ int ntc_gf_combine_batch(ntc_gf256_engine* e, uint32_t w, uint32_t G, uint32_t k
   CombineArgs a{G, k, rows, stride, in, coef, out};
   using Fn = void (*)(CombineArgs, uint32_t, uint32_t);
   Fn fn;
-  switch (w * 16 + rb) {
-#define NTC_GFW_CASE(W_, RB_) case W_ * 16 + RB_: fn = fr ? gfw_combine_fr<W_, RB_> : gfw_combine<W_, RB_>; break;
-    NTC_GFW_CASE(4, 1) NTC_GFW_CASE(4, 2) NTC_GFW_CASE(4, 4) NTC_GFW_CASE(4, 8)
-    NTC_GFW_CASE(8, 1) NTC_GFW_CASE(8, 2) NTC_GFW_CASE(8, 4) NTC_GFW_CASE(8, 8)
-    NTC_GFW_CASE(16, 1) NTC_GFW_CASE(16, 2) NTC_GFW_CASE(16, 4) NTC_GFW_CASE(16, 8)
-    NTC_GFW_CASE(32, 1) NTC_GFW_CASE(32, 2) NTC_GFW_CASE(32, 4) NTC_GFW_CASE(32, 8)
+  switch (w * 32 + rb) {
+#define NTC_GFW_CASE(W_, RB_) case W_ * 32 + RB_: fn = fr ? gfw_combine_fr<W_, RB_> : gfw_combine<W_, RB_>; break;
+#define NTC_GFW_CASE16(W_) case W_ * 32 + 16: fn = gfw_combine_fr<W_, 16>; break;
+    NTC_GFW_CASE(4, 1) NTC_GFW_CASE(4, 2) NTC_GFW_CASE(4, 4) NTC_GFW_CASE(4, 8) NTC_GFW_CASE16(4)
+    NTC_GFW_CASE(8, 1) NTC_GFW_CASE(8, 2) NTC_GFW_CASE(8, 4) NTC_GFW_CASE(8, 8) NTC_GFW_CASE16(8)
+    NTC_GFW_CASE(16, 1) NTC_GFW_CASE(16, 2) NTC_GFW_CASE(16, 4) NTC_GFW_CASE(16, 8) NTC_GFW_CASE16(16)
+    NTC_GFW_CASE(32, 1) NTC_GFW_CASE(32, 2) NTC_GFW_CASE(32, 4) NTC_GFW_CASE(32, 8) NTC_GFW_CASE16(32)
 #undef NTC_GFW_CASE
+#undef NTC_GFW_CASE16
     default: return fail(NTC_GPU_EINVAL, "w must be 4, 8, 16 or 32");
   }
   hipLaunchKernelGGL(fn, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0,

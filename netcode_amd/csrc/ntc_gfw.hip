@@ -259,9 +259,10 @@ __global__ __launch_bounds__(256) void gfw_combine_fr(CombineArgs a, uint32_t ns
   };
   uint32_t cn[RB];
   coefs(0, cn);
-  const typename std::conditional<(W >= 16), XtimeV<W>, XtimeC<W>>::type xtv;
+  // (16 rows: the constant forms, whose operands need no VGPRs -- measured as fast at 8 rows)
+  const typename std::conditional<(W >= 16 && RB < 16), XtimeV<W>, XtimeC<W>>::type xtv;
   // inputs PF ahead in registers (a wave's work per input is short next to the memory latency)
-  constexpr int PF = D == 4 ? 2 : 3;
+  constexpr int PF = RB == 16 && D == 2 ? 1 : D == 4 ? 2 : 3;   // (w = 16 x 16 rows: 3 waves per SIMD need <= 168 VGPRs)
   V nx[PF];
 #pragma unroll
   for (int j = 0; j < PF; ++j)
